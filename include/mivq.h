@@ -1,0 +1,167 @@
+/*
+ * mivq.h — C ABI of libmivq.so, the MI355X-native (gfx950) vector-quantization hot path.
+ *
+ * This is the drop-in boundary that replaces the faiss / numpy calls the reference's
+ * quantizer classes make (citations are /root/reference/<path>:<line>).  Every entry
+ * point is `extern "C"`, takes plain pointers and sizes, and is stream-ordered:
+ *
+ *   - Ownership: every buffer is caller-allocated DEVICE memory (e.g. a torch tensor's
+ *     data_ptr()).  The library never allocates persistent memory; kernels that need
+ *     scratch take an explicit workspace (size from the matching *_workspace_bytes()).
+ *   - Errors: 0 on success, a negative MIVQ_ERR_* code otherwise; the message is kept in
+ *     a thread-local buffer readable with mivq_last_error().  The Python host raises the
+ *     same exception types the reference raises (AssertionError / ValueError /
+ *     RuntimeError, see vector-quantization_amd/haag_vq/_native.py).
+ *   - Threading: asynchronous on `stream` (a hipStream_t passed as void*; NULL = the
+ *     legacy default stream of the current device).  Safe to call concurrently from
+ *     several host threads on different streams or devices; no global mutable state
+ *     besides the per-thread error string.  No call synchronises the device.
+ *   - Codes: PQ codes follow faiss' ProductQuantizer layout (code_size = ceil(M*nbits/8)
+ *     bytes per vector, sub-code m in bits [m*nbits, (m+1)*nbits) of the little-endian
+ *     bit stream; nbits == 8 is one byte per subspace).  Centroids are laid out
+ *     (M, ksub, dsub) f32, exactly `pq.centroids.reshape(M, ksub, dsub)` of
+ *     product_quantization.py:72-73.
+ */
+#ifndef MIVQ_H
+#define MIVQ_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+#pragma GCC visibility push(default)
+
+#define MIVQ_OK 0
+#define MIVQ_ERR_INVALID (-1)     /* bad shape / argument            -> ValueError / AssertionError */
+#define MIVQ_ERR_UNSUPPORTED (-2) /* configuration not implemented   -> ValueError */
+#define MIVQ_ERR_HIP (-3)         /* HIP runtime / launch failure    -> RuntimeError */
+#define MIVQ_ERR_WORKSPACE (-4)   /* workspace too small             -> RuntimeError */
+
+#define MIVQ_ABI_VERSION 1
+
+/* PQ encode flags */
+#define MIVQ_PQ_AUTO 0u        /* fp16-MFMA candidate filter + exact fp32 re-check when supported */
+#define MIVQ_PQ_FORCE_EXACT 1u /* exact fp32 VALU scan of every centroid (canonical order)     */
+
+/* Metric enum values follow faiss / haag_vq.utils.faiss_utils.MetricType (faiss_utils.py:3-5). */
+#define MIVQ_METRIC_INNER_PRODUCT 0
+#define MIVQ_METRIC_L2 1
+
+/* ---------------------------------------------------------------- misc */
+const char* mivq_last_error(void);
+int mivq_abi_version(void);
+/* Fills name (>= 64 bytes), compute units, LDS bytes per CU, and total HBM bytes of `device`. */
+int mivq_device_info(int device, char* name, int32_t* cus, int64_t* lds_per_cu, int64_t* hbm_bytes);
+
+/* ------------------------------------------------------ product quantizer
+ * Replaces faiss.ProductQuantizer.compute_codes / decode behind
+ * ProductQuantizer.compress / decompress (product_quantization.py:76-86).
+ *
+ * Canonical encode (what "bit-exact" is measured against, see oracle/mivq_oracle.c):
+ *   cn[m][k]  = fmaf-chain over t ascending of c[m][k][t]^2
+ *   dot       = fmaf-chain over t ascending of x[m*dsub+t] * c[m][k][t]   (starts at +0)
+ *   score_k   = fl32(cn[m][k] - 2*dot)
+ *   code[m]   = smallest k with the minimum score (scores that are NaN never win; an
+ *               all-NaN row gives 0).
+ */
+
+/* Bytes of the derived codebook data ("prep") for mivq_pq_encode. */
+size_t mivq_pq_prep_bytes(int32_t d, int32_t M, int32_t nbits);
+/* Builds prep from centroids (device): canonical norms, the fp16 MFMA operand image and
+ * the per-subspace rounding-bound constants.  Re-run whenever the centroids change. */
+int mivq_pq_prepare(const float* centroids, int32_t d, int32_t M, int32_t nbits, void* prep,
+                    void* stream);
+size_t mivq_pq_encode_workspace_bytes(int64_t n, int32_t d, int32_t M, int32_t nbits);
+/* x: (n, d) f32 row-major; codes: (n, code_size) u8; prep from mivq_pq_prepare (required;
+ * the exact path reads its canonical norms and transposed codebook). */
+int mivq_pq_encode(const float* x, int64_t n, int32_t d, int32_t M, int32_t nbits,
+                   const float* centroids, const void* prep, void* workspace,
+                   size_t workspace_bytes, uint8_t* codes, uint32_t flags, void* stream);
+/* out: (n, d) f32: out[i, m*dsub:(m+1)*dsub] = centroids[m, code_m(i), :]. */
+int mivq_pq_decode(const uint8_t* codes, int64_t n, int32_t d, int32_t M, int32_t nbits,
+                   const float* centroids, float* out, void* stream);
+/* faiss bit-stream <-> one byte per sub-code (identity copy for nbits == 8). */
+int mivq_pq_unpack(const uint8_t* codes, int64_t n, int32_t M, int32_t nbits, uint8_t* out,
+                   void* stream);
+
+/* ---------------------------------------------------- k-means (PQ fit)
+ * Deterministic centroid update for the per-subspace Lloyd iterations that replace
+ * faiss' ProductQuantizer.train (product_quantization.py:67-68): sums[m][k][t] are
+ * accumulated over assigned rows in ascending row order, centroids = sums / count for
+ * non-empty clusters (empty clusters keep their previous value and report count 0).
+ * assign: (n, M) u8 (one byte per subspace, the output of mivq_pq_encode with nbits 8
+ * or of mivq_pq_unpack).  counts: (M, ksub) int32. */
+int mivq_kmeans_update(const float* x, int64_t n, int32_t d, int32_t M, int32_t ksub,
+                       const uint8_t* assign, float* centroids, int32_t* counts, void* stream);
+
+/* ------------------------------------------------------ OPQ rotation
+ * Replaces faiss.OPQMatrix.apply / reverse_transform
+ * (optimized_product_quantization.py:26,31,34).  A is (d, d) f32 row-major.
+ *   transpose == 0 : y = x . A^T   (apply)
+ *   transpose == 1 : y = x . A     (reverse_transform of an orthonormal A) */
+int mivq_opq_rotate(const float* x, int64_t n, int32_t d, const float* A, int32_t transpose,
+                    float* y, void* stream);
+
+/* ------------------------------------------------------ scalar quantizer
+ * Replaces ScalarQuantizer._compress_block / decompress (scalar_quantization.py:52-90)
+ * bit-for-bit, in the dtype numpy would compute in (f32 input -> f32 math, f64 -> f64).
+ *   lo  = X.min(0), den = (X.max(0) - X.min(0)) + 1e-8 (computed by the caller exactly as
+ *   numpy does); codes: u8 for nbits 4 (two dims per byte, even dim in the high nibble,
+ *   odd d zero-padded) and 8, u16 for nbits 16.  Decode returns f32 for the f32 variant
+ *   and f64 for the f64 variant (what numpy returns). */
+int mivq_sq_encode_f32(const float* x, int64_t n, int32_t d, const float* lo, const float* den,
+                       int32_t nbits, void* codes, void* stream);
+int mivq_sq_encode_f64(const double* x, int64_t n, int32_t d, const double* lo,
+                       const double* den, int32_t nbits, void* codes, void* stream);
+int mivq_sq_decode_f32(const void* codes, int64_t n, int32_t d, const float* lo,
+                       const float* den, int32_t nbits, float* out, void* stream);
+int mivq_sq_decode_f64(const void* codes, int64_t n, int32_t d, const double* lo,
+                       const double* den, int32_t nbits, double* out, void* stream);
+
+/* ------------------------------------------------------ RaBitQ (1 bit)
+ * Replaces faiss.RaBitQuantizer.compute_codes / decode (rabit_quantization.py:20-29).
+ * Code row = ceil(d/8) sign bytes (bit j of dim j = (x_j - c_j) > 0, LSB-first) followed by
+ * two f32 factors {||x-c||^2, dp_multiplier}; code_size = ceil(d/8) + 8.
+ * centroid may be NULL (faiss' default: no centroid). */
+int mivq_rabitq_encode(const float* x, int64_t n, int32_t d, const float* centroid,
+                       int32_t metric, uint8_t* codes, void* stream);
+int mivq_rabitq_decode(const uint8_t* codes, int64_t n, int32_t d, const float* centroid,
+                       float* out, void* stream);
+
+/* ------------------------------------------------------ ADC search
+ * Flat asymmetric-distance search over PQ codes; the GPU counterpart of
+ * FlatQuantizedIndex.search_with_scores (methods/search/flat_quantized_index.py:45-76),
+ * which decodes every code and ranks exact distances to the reconstructions.
+ *   lut[q][m][k] = sum over t ascending of (q[m*dsub+t] - c[m][k][t])^2 (fmaf chain), or for
+ *                  metric == MIVQ_METRIC_INNER_PRODUCT  -(fmaf chain of q * c)
+ *   dist(q, i)   = ((lut[q][0][code_0] + lut[q][1][code_1]) + ...) + lut[q][M-1][code_M-1]
+ * Results per query are the k smallest (dist, id) pairs in ascending (dist, id) order
+ * (ties broken by the smaller global id = id_offset + row); missing slots (n < k) hold
+ * dist = +inf, id = 0xFFFFFFFF. */
+int mivq_adc_lut(const float* q, int64_t nq, int32_t d, int32_t M, int32_t nbits,
+                 const float* centroids, int32_t metric, float* lut, void* stream);
+size_t mivq_adc_search_workspace_bytes(int64_t nq, int64_t n, int32_t M, int32_t nbits, int32_t k);
+/* codes: (n, M) one byte per sub-code (nbits <= 8; use mivq_pq_unpack for nbits < 8). */
+int mivq_adc_search(const float* lut, int64_t nq, const uint8_t* codes, int64_t n, int32_t M,
+                    int32_t nbits, int32_t k, int64_t id_offset, void* workspace,
+                    size_t workspace_bytes, float* dists, uint32_t* ids, void* stream);
+/* Exact brute-force top-k over an f32 database (the decode-then-search path of
+ * FlatQuantizedIndex for SQ / RaBitQ reconstructions, flat_quantized_index.py:57-76):
+ *   L2: dist = fmaf chain over t of (q_t - x_t)^2;  IP: dist = -(fmaf chain of q_t * x_t)
+ * ranked ascending by (dist, id) exactly like mivq_adc_search (callers negate IP back). */
+size_t mivq_flat_search_workspace_bytes(int64_t nq, int64_t n, int32_t d, int32_t k);
+int mivq_flat_search(const float* q, int64_t nq, const float* x, int64_t n, int32_t d,
+                     int32_t metric, int32_t k, int64_t id_offset, void* workspace,
+                     size_t workspace_bytes, float* dists, uint32_t* ids, void* stream);
+/* Merges `parts` sorted (nq, k) lists laid out (parts, nq, k) into one sorted (nq, k) list
+ * with the same (dist, id) order — the on-device merge after the RCCL all-gather. */
+int mivq_topk_merge(const float* dists_in, const uint32_t* ids_in, int32_t parts, int64_t nq,
+                    int32_t k, float* dists_out, uint32_t* ids_out, void* stream);
+
+#pragma GCC visibility pop
+#ifdef __cplusplus
+}
+#endif
+#endif /* MIVQ_H */

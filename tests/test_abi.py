@@ -1,0 +1,70 @@
+"""CPU: libmivq.so builds, loads and exports exactly the C ABI declared in include/mivq.h."""
+
+import re
+from pathlib import Path
+
+import pytest
+
+ROOT = Path(__file__).resolve().parents[1]
+
+
+def _declared():
+    txt = (ROOT / "include" / "mivq.h").read_text()
+    txt = re.sub(r"/\*.*?\*/", "", txt, flags=re.S)
+    return sorted(set(re.findall(r"\b(mivq_[a-z0-9_]+)\s*\(", txt)))
+
+
+def test_header_declares_the_boundary():
+    names = _declared()
+    for must in ("mivq_pq_encode", "mivq_pq_decode", "mivq_opq_rotate", "mivq_sq_encode_f32",
+                 "mivq_rabitq_encode", "mivq_adc_lut", "mivq_adc_search", "mivq_topk_merge",
+                 "mivq_last_error", "mivq_device_info"):
+        assert must in names
+
+
+def test_library_exports_every_declared_symbol():
+    from haag_vq import _native
+
+    lib = _native.load_library()
+    for name in _declared():
+        assert hasattr(lib, name), name
+    assert set(_declared()) == set(_native.SIGNATURES), "ctypes table out of sync with mivq.h"
+    assert lib.mivq_abi_version() == 1
+
+
+def test_size_queries_need_no_gpu():
+    from haag_vq import _native
+
+    lib = _native.load_library()
+    assert lib.mivq_pq_prep_bytes(1536, 16, 8) > 16 * 256 * 4
+    assert lib.mivq_pq_prep_bytes(1000, 16, 8) == 0  # D % M != 0
+    assert lib.mivq_pq_encode_workspace_bytes(1000, 1536, 16, 8) > 0
+    assert lib.mivq_adc_search_workspace_bytes(100, 10000, 16, 8, 10) > 0
+
+
+def test_error_path_needs_no_gpu():
+    """Argument validation happens before any HIP call and maps to the reference's exceptions."""
+    from haag_vq import _native
+
+    lib = _native.load_library()
+    rc = lib.mivq_pq_encode(None, 10, 1000, 16, 8, None, None, None, 0, None, 0, None)
+    assert rc == _native.MIVQ_ERR_INVALID
+    assert b"divisible" in lib.mivq_last_error()
+    with pytest.raises(AssertionError):
+        _native._raise(rc)
+    rc = lib.mivq_sq_encode_f32(None, 1, 4, None, None, 5, None, None)
+    assert rc == _native.MIVQ_ERR_INVALID
+    with pytest.raises(ValueError):
+        _native._raise(rc)
+
+
+def test_compute_without_gpu_fails_loudly():
+    import torch
+
+    if torch.cuda.is_available():
+        pytest.skip("GPU present")
+    from haag_vq.methods.product_quantization import ProductQuantizer
+
+    pq = ProductQuantizer(M=4, B=8)
+    with pytest.raises(RuntimeError, match="no CPU fallback"):
+        pq.fit([[0.0] * 8] * 300)

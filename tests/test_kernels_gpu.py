@@ -1,0 +1,279 @@
+"""GPU parity: every libmivq entry point against the CPU oracle (bit-exact where the
+contract says so), called through the C ABI binding (haag_vq._native)."""
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+torch = pytest.importorskip("torch")
+
+
+def _t(a, dev):
+    return torch.from_numpy(np.ascontiguousarray(a)).to(dev)
+
+
+def _h(t):
+    return t.detach().cpu().numpy()
+
+
+def _codebook(rng, X, M, ksub, dups=True):
+    """Centroids drawn from data rows + noise, with exact duplicates and near-duplicates."""
+    n, d = X.shape
+    dsub = d // M
+    idx = rng.integers(0, n, size=ksub)
+    C = X[idx].reshape(ksub, M, dsub).transpose(1, 0, 2).copy()
+    C += rng.standard_normal(C.shape).astype(np.float32) * 0.05 * np.abs(C).mean()
+    if dups and ksub >= 8:
+        C[:, 5] = C[:, 3]                    # exact tie: canonical first index wins
+        C[:, 7] = C[:, 6] * (1 + 1e-7)       # near tie
+    return np.ascontiguousarray(C, dtype=np.float32)
+
+
+PQ_SHAPES = [
+    # n, d, M, nbits          path
+    (1000, 1536, 16, 8),    # MFMA KS=6 (the headline shape)
+    (777, 1024, 16, 8),     # MFMA KS=4, ragged n
+    (513, 1536, 32, 8),     # MFMA KS=3 (OPQ32 shape)
+    (300, 1024, 8, 8),      # MFMA KS=8 (dsub 128)
+    (300, 1536, 8, 8),      # dsub 192 -> exact path
+    (200, 48, 6, 8),        # dsub 8, KS=1
+    (257, 48, 12, 8),       # dsub 4
+    (256, 16, 4, 4),        # nbits 4 (faiss bit stream)
+    (100, 30, 10, 3),       # dsub 3, nbits 3 -> exact path + pack
+    (64, 64, 8, 1),         # nbits 1
+    (1, 1536, 16, 8),       # single row
+]
+
+
+@pytest.mark.parametrize("n,d,M,nbits", PQ_SHAPES)
+def test_pq_encode_bit_exact(dev, oracle, n, d, M, nbits):
+    from haag_vq import _native
+
+    rng = np.random.default_rng(n * 7 + d + M)
+    X = rng.standard_normal((n, d)).astype(np.float32)
+    X /= np.linalg.norm(X, axis=1, keepdims=True)
+    Xtrain = rng.standard_normal((max(n, 1 << nbits), d)).astype(np.float32)
+    Xtrain /= np.linalg.norm(Xtrain, axis=1, keepdims=True)
+    C = _codebook(rng, Xtrain, M, 1 << nbits)
+    # rows that sit exactly on centroids / between tied centroids
+    if n > 10 and nbits >= 3:
+        X[3] = C[:, 3].reshape(-1)
+        X[4] = 0.5 * (C[:, 6] + C[:, 7]).reshape(-1)
+    ref = oracle.pq_pack(oracle.pq_encode(X, C), nbits)
+    Cd = _t(C, dev)
+    prep = _native.pq_prepare(Cd, nbits)
+    got = _h(_native.pq_encode(_t(X, dev), Cd, prep, nbits))
+    np.testing.assert_array_equal(got, ref)
+    got_exact = _h(_native.pq_encode(_t(X, dev), Cd, prep, nbits, exact=True))
+    np.testing.assert_array_equal(got_exact, ref)
+
+
+def test_pq_encode_extreme_rows_fall_back_exactly(dev, oracle):
+    """fp16 overflow (huge rows), NaN rows and zero rows take the exact fallback."""
+    from haag_vq import _native
+
+    rng = np.random.default_rng(5)
+    n, d, M = 300, 1536, 16
+    X = rng.standard_normal((n, d)).astype(np.float32)
+    C = _codebook(rng, X, M, 256)
+    X[10] *= 1e6
+    X[11] = 0.0
+    X[12, :5] = np.nan
+    X[13] *= 1e-12
+    ref = oracle.pq_encode(X, C)
+    Cd = _t(C, dev)
+    prep = _native.pq_prepare(Cd, 8)
+    got = _h(_native.pq_encode(_t(X, dev), Cd, prep, 8))
+    np.testing.assert_array_equal(got, ref)
+
+
+def test_pq_encode_matches_fp64_on_clear_cases(dev, oracle):
+    from haag_vq import _native
+
+    rng = np.random.default_rng(9)
+    X = rng.standard_normal((400, 1536)).astype(np.float32)
+    C = _codebook(rng, X, 16, 256, dups=False)
+    codes64, gap = oracle.pq_encode_fp64(X, C)
+    Cd = _t(C, dev)
+    got = _h(_native.pq_encode(_t(X, dev), Cd, _native.pq_prepare(Cd, 8), 8))
+    clear = gap > 1e-5
+    assert clear.mean() > 0.9
+    np.testing.assert_array_equal(got[clear], codes64[clear])
+
+
+@pytest.mark.parametrize("n,d,M,nbits", [(300, 1536, 16, 8), (256, 16, 4, 4), (100, 30, 10, 3)])
+def test_pq_decode_bit_exact(dev, oracle, n, d, M, nbits):
+    from haag_vq import _native
+
+    rng = np.random.default_rng(1)
+    C = rng.standard_normal((M, 1 << nbits, d // M)).astype(np.float32)
+    u8 = rng.integers(0, 1 << nbits, size=(n, M)).astype(np.uint8)
+    packed = oracle.pq_pack(u8, nbits)
+    ref = oracle.pq_decode(u8, C)
+    got = _h(_native.pq_decode(_t(packed, dev), _t(C, dev), nbits))
+    np.testing.assert_array_equal(got, ref)
+    np.testing.assert_array_equal(_h(_native.pq_unpack(_t(packed, dev), M, nbits)), u8)
+
+
+def test_pq_encode_empty(dev):
+    from haag_vq import _native
+
+    C = torch.zeros((16, 256, 96), device=dev)
+    prep = _native.pq_prepare(C, 8)
+    out = _native.pq_encode(torch.zeros((0, 1536), device=dev), C, prep, 8)
+    assert tuple(out.shape) == (0, 16)
+
+
+def test_pq_errors(dev):
+    from haag_vq import _native
+
+    C = torch.zeros((16, 256, 96), device=dev)
+    with pytest.raises(ValueError):
+        _native.pq_encode(torch.zeros((4, 1000), device=dev), C, _native.pq_prepare(C, 8), 8)
+    with pytest.raises(ValueError):
+        _native.pq_prepare(torch.zeros((16, 100, 96), device=dev), 8)
+
+
+def test_sq_golden_bit_exact(dev, golden_dir):
+    from haag_vq import _native
+
+    g = np.load(golden_dir / "sq_golden.npz")
+    for tag in g["cases"]:
+        tag = str(tag)
+        X, lo, hi, codes, recon = (g[f"{tag}_{k}"] for k in ("X", "lo", "hi", "codes", "recon"))
+        bits = int(tag.split("_b")[1])
+        den = (hi - lo) + 1e-8
+        c = _h(_native.sq_encode(_t(X, dev), _t(lo, dev), _t(den, dev), bits))
+        if bits == 16:
+            c = c.view(np.uint16)
+        np.testing.assert_array_equal(c, codes, err_msg=tag)
+        ct = _t(codes.view(np.int16) if bits == 16 else codes, dev)
+        r = _h(_native.sq_decode(ct, X.shape[1], _t(lo, dev), _t(den, dev), bits))
+        assert r.dtype == recon.dtype, tag
+        np.testing.assert_array_equal(r.view(np.uint8), recon.view(np.uint8), err_msg=tag)
+
+
+@pytest.mark.parametrize("n,d", [(500, 1024), (333, 3072), (77, 37)])
+@pytest.mark.parametrize("metric", [1, 0])
+def test_rabitq_parity(dev, oracle, n, d, metric):
+    from haag_vq import _native
+
+    rng = np.random.default_rng(d)
+    X = rng.standard_normal((n, d)).astype(np.float32)
+    X[0] = 0.0  # degenerate row (epsilon guards)
+    ref = oracle.rabitq_encode(X, metric=metric)
+    got = _h(_native.rabitq_encode(_t(X, dev), None, metric))
+    nb = (d + 7) // 8
+    np.testing.assert_array_equal(got[:, :nb], ref[:, :nb])
+    f_ref = ref[:, nb:].copy().view(np.float32)
+    f_got = got[:, nb:].copy().view(np.float32)
+    np.testing.assert_allclose(f_got, f_ref, rtol=1e-5, atol=1e-5 * np.abs(f_ref).max())
+    rec = _h(_native.rabitq_decode(_t(got, dev), d, None))
+    np.testing.assert_array_equal(rec, oracle.rabitq_decode(got, d))  # same code row -> same floats
+
+
+@pytest.mark.parametrize("nq,n,d,M,nbits,k", [
+    (37, 5000, 1536, 16, 8, 10),
+    (9, 3000, 1536, 32, 8, 100),
+    (16, 1000, 64, 8, 4, 7),
+    (5, 200, 48, 6, 8, 256),
+    (3, 5, 64, 8, 8, 10),   # fewer rows than k: sentinel slots
+])
+@pytest.mark.parametrize("metric", [1, 0])
+def test_adc_bit_exact(dev, oracle, nq, n, d, M, nbits, k, metric):
+    from haag_vq import _native
+
+    rng = np.random.default_rng(nq + n)
+    C = rng.standard_normal((M, 1 << nbits, d // M)).astype(np.float32)
+    Q = rng.standard_normal((nq, d)).astype(np.float32)
+    u8 = rng.integers(0, 1 << nbits, size=(n, M)).astype(np.uint8)
+    u8[1] = u8[0]  # duplicate rows: equal distances, id tie-break
+    lut_ref = oracle.adc_lut(Q, C, metric)
+    lut = _native.adc_lut(_t(Q, dev), _t(C, dev), nbits, metric)
+    np.testing.assert_array_equal(_h(lut), lut_ref)
+    d_ref, i_ref = oracle.adc_search(lut_ref, u8, k)
+    dd, ii = _native.adc_search(lut, _t(u8, dev), k, nbits)
+    np.testing.assert_array_equal(_h(dd), d_ref)
+    np.testing.assert_array_equal(_h(ii).view(np.uint32), i_ref)
+
+
+@pytest.mark.parametrize("nq,n,d,k", [(20, 3000, 1024, 10), (7, 500, 37, 100), (4, 3, 16, 5)])
+@pytest.mark.parametrize("metric", [1, 0])
+def test_flat_search_bit_exact(dev, oracle, nq, n, d, k, metric):
+    from haag_vq import _native
+
+    rng = np.random.default_rng(d)
+    X = rng.standard_normal((n, d)).astype(np.float32)
+    Q = rng.standard_normal((nq, d)).astype(np.float32)
+    d_ref, i_ref = oracle.flat_search(Q, X, k, metric)
+    dd, ii = _native.flat_search(_t(Q, dev), _t(X, dev), k, metric)
+    np.testing.assert_array_equal(_h(dd), d_ref)
+    np.testing.assert_array_equal(_h(ii).view(np.uint32), i_ref)
+
+
+def test_sharded_adc_merge_equals_single(dev, oracle):
+    """Row shards searched with id offsets and merged == one search (multi-GPU contract)."""
+    from haag_vq import _native
+
+    rng = np.random.default_rng(3)
+    nq, n, M, k = 11, 4000, 16, 10
+    C = rng.standard_normal((M, 256, 8)).astype(np.float32)
+    Q = rng.standard_normal((nq, M * 8)).astype(np.float32)
+    u8 = rng.integers(0, 256, size=(n, M)).astype(np.uint8)
+    lut = _native.adc_lut(_t(Q, dev), _t(C, dev), 8)
+    full_d, full_i = _native.adc_search(lut, _t(u8, dev), k, 8)
+    for parts in (2, 3, 8):
+        bounds = np.linspace(0, n, parts + 1).astype(int)
+        ds, is_ = [], []
+        for a, b in zip(bounds[:-1], bounds[1:]):
+            d_, i_ = _native.adc_search(lut, _t(u8[a:b], dev), k, 8, id_offset=int(a))
+            ds.append(d_)
+            is_.append(i_)
+        md, mi = _native.topk_merge(torch.stack(ds).contiguous(), torch.stack(is_).contiguous(), k)
+        np.testing.assert_array_equal(_h(md), _h(full_d))
+        np.testing.assert_array_equal(_h(mi), _h(full_i))
+
+
+def test_opq_rotate(dev):
+    from haag_vq import _native
+
+    rng = np.random.default_rng(4)
+    for n, d in ((1000, 1536), (130, 100), (7, 48)):
+        X = rng.standard_normal((n, d)).astype(np.float32)
+        A = np.linalg.qr(rng.standard_normal((d, d)))[0].astype(np.float32)
+        y = _h(_native.opq_rotate(_t(X, dev), _t(A, dev), False))
+        ref = X.astype(np.float64) @ A.astype(np.float64).T
+        tol = 1e-5 * np.linalg.norm(X, axis=1, keepdims=True)
+        assert np.all(np.abs(y - ref) <= tol + 1e-30)
+        back = _h(_native.opq_rotate(_t(y, dev), _t(A, dev), True))
+        ref2 = y.astype(np.float64) @ A.astype(np.float64)
+        assert np.all(np.abs(back - ref2) <= tol + 1e-30)
+
+
+def test_kmeans_update_deterministic(dev):
+    from haag_vq import _native
+
+    rng = np.random.default_rng(8)
+    n, M, ksub, dsub = 5000, 4, 16, 8
+    X = rng.standard_normal((n, M * dsub)).astype(np.float32)
+    assign = rng.integers(0, ksub - 1, size=(n, M)).astype(np.uint8)  # last cluster empty
+    C0 = rng.standard_normal((M, ksub, dsub)).astype(np.float32)
+    Cd = _t(C0, dev)
+    counts = torch.empty((M, ksub), dtype=torch.int32, device=dev)
+    _native.kmeans_update(_t(X, dev), _t(assign, dev), Cd, counts)
+    C = _h(Cd)
+    cnt = _h(counts)
+    Xs = X.reshape(n, M, dsub)
+    for m in range(M):
+        for k in range(ksub):
+            sel = assign[:, m] == k
+            assert cnt[m, k] == sel.sum()
+            if sel.sum():
+                # ascending-row sequential f32 sum, then one division
+                s = np.zeros(dsub, np.float32)
+                for row in np.nonzero(sel)[0]:
+                    s = (s + Xs[row, m]).astype(np.float32)
+                np.testing.assert_array_equal(C[m, k], (s / np.float32(sel.sum())).astype(np.float32))
+            else:
+                np.testing.assert_array_equal(C[m, k], C0[m, k])

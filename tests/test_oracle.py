@@ -1,0 +1,130 @@
+"""CPU: the oracle is pinned against the reference's own fixtures and logged KATs."""
+
+import json
+
+import numpy as np
+import pytest
+
+
+def test_sq_oracle_matches_reference_fixtures(oracle, golden_dir):
+    g = np.load(golden_dir / "sq_golden.npz")
+    assert len(g["cases"]) == 18
+    for tag in g["cases"]:
+        tag = str(tag)
+        X, lo, hi, codes, recon = (g[f"{tag}_{k}"] for k in ("X", "lo", "hi", "codes", "recon"))
+        bits = int(tag.split("_b")[1])
+        den = hi - lo + 1e-8
+        c = oracle.sq_encode(X, lo, den, bits)
+        np.testing.assert_array_equal(c, codes, err_msg=tag)
+        r = oracle.sq_decode(c, X.shape[1], lo, den, bits)
+        assert r.dtype == recon.dtype
+        np.testing.assert_array_equal(r.view(np.uint8), recon.view(np.uint8), err_msg=tag)
+
+
+def test_extrabitq_oracle_matches_reference_fixtures(oracle, golden_dir):
+    e = np.load(golden_dir / "extrabitq_golden.npz")
+    X = e["X"]
+    for tag in e["cases"]:
+        tag = str(tag)
+        b = int(tag[1:])
+        c, P, lv = oracle.extrabitq_fit(X, b)
+        np.testing.assert_array_equal(c, e[f"{tag}_c"])
+        np.testing.assert_array_equal(P, e[f"{tag}_P"])
+        np.testing.assert_array_equal(lv, e[f"{tag}_levels"])
+        codes = oracle.extrabitq_encode(X, c, P, lv, b)
+        np.testing.assert_array_equal(codes, e[f"{tag}_codes"])
+        np.testing.assert_array_equal(oracle.extrabitq_decode(codes, c, P, lv, b), e[f"{tag}_recon"])
+
+
+@pytest.fixture(scope="module")
+def dummy():
+    """load_dummy_dataset(): np.random.seed(42); randn(10000, 1024) (datasets.py:79-81)."""
+    np.random.seed(42)
+    return np.random.randn(10000, 1024)
+
+
+@pytest.fixture(scope="module")
+def kat(golden_dir):
+    return json.loads((golden_dir / "kat.json").read_text())
+
+
+def _recall(gt, ret, k):
+    return sum(len(set(gt[i, :k]) & set(ret[i, :k])) / k for i in range(len(gt))) / len(gt)
+
+
+def test_sq8_kat_row38(oracle, dummy, kat):
+    m = kat["38"]["metrics"]
+    lo, hi, den = oracle.sq_fit(dummy)
+    rec = oracle.sq_decode(oracle.sq_encode(dummy, lo, den, 8), 1024, lo, den, 8)
+    dist = np.mean(np.sum((dummy - rec) ** 2, axis=1))
+    # codes/reconstructions are bit-exact (fixtures); the logged fp64 mean differs by 1 ulp
+    # (numpy's pairwise-summation blocking on the logging machine)
+    assert abs(dist - m["reconstruction_distortion"]) <= 2 * np.spacing(m["reconstruction_distortion"])
+    gt = oracle.exact_l2_topk(dummy[:100], dummy, 100)
+    from sklearn.metrics import pairwise_distances
+
+    ret = pairwise_distances(dummy[:100], rec).argsort(axis=1)
+    assert _recall(gt, ret, 10) == pytest.approx(m["recall@10"], abs=1e-12)
+    assert _recall(gt, ret, 100) == pytest.approx(m["recall@100"], abs=1e-12)
+
+
+def test_rabitq_kat_row52(oracle, dummy, kat):
+    m = kat["52"]["metrics"]
+    codes = oracle.rabitq_encode(dummy.astype(np.float32))
+    assert 4096 / codes.shape[1] == pytest.approx(m["compression_ratio"])
+    rec = oracle.rabitq_decode(codes, 1024)
+    dist = np.mean(np.sum((dummy - rec) ** 2, axis=1))
+    assert dist == pytest.approx(m["reconstruction_distortion"], rel=1e-7)
+    gt = oracle.exact_l2_topk(dummy[:100], dummy, 100)
+    from sklearn.metrics import pairwise_distances
+
+    ret = pairwise_distances(dummy[:100], rec).argsort(axis=1)
+    assert _recall(gt, ret, 10) == pytest.approx(m["recall@10"], abs=1e-12)
+    assert _recall(gt, ret, 100) == pytest.approx(m["recall@100"], abs=1e-12)
+
+
+def test_pq_oracle_agrees_with_fp64_nearest_centroid(oracle):
+    """Parity of the canonical PQ encode is unpinned vs faiss; any correct nearest-centroid
+    implementation must agree with fp64 brute force wherever the top-2 gap is clear."""
+    rng = np.random.default_rng(0)
+    X = rng.standard_normal((600, 96)).astype(np.float32)
+    C = rng.standard_normal((4, 256, 24)).astype(np.float32)
+    codes = oracle.pq_encode(X, C)
+    c64, gap = oracle.pq_encode_fp64(X, C)
+    clear = gap > 1e-6
+    assert clear.mean() > 0.95
+    np.testing.assert_array_equal(codes[clear], c64[clear])
+
+
+def test_pq_oracle_first_index_tie_break(oracle):
+    C = np.zeros((1, 8, 4), np.float32)
+    C[0, 2] = [1, 0, 0, 0]
+    C[0, 5] = [1, 0, 0, 0]
+    X = np.array([[1, 0, 0, 0], [0, 0, 0, 0], [np.nan, 0, 0, 0]], np.float32)
+    codes = oracle.pq_encode(X, C)
+    assert codes[:, 0].tolist() == [2, 0, 0]
+
+
+def test_pq_pack_roundtrip(oracle):
+    rng = np.random.default_rng(1)
+    for M, nbits in ((8, 8), (4, 4), (10, 3), (7, 1), (5, 6)):
+        u8 = rng.integers(0, 1 << nbits, size=(50, M)).astype(np.uint8)
+        packed = oracle.pq_pack(u8, nbits)
+        assert packed.shape[1] == (M * nbits + 7) // 8
+        np.testing.assert_array_equal(oracle.pq_unpack(packed, M, nbits), u8)
+    # faiss layout: sub-code m in bits [m*nbits, (m+1)*nbits), LSB first
+    p = oracle.pq_pack(np.array([[1, 2]], np.uint8), 4)
+    assert p.tolist() == [[0x21]]
+
+
+def test_adc_oracle_equals_decode_then_exact(oracle):
+    rng = np.random.default_rng(2)
+    M, ksub, dsub = 4, 16, 8
+    C = rng.standard_normal((M, ksub, dsub)).astype(np.float32)
+    codes = rng.integers(0, ksub, size=(300, M)).astype(np.uint8)
+    Q = rng.standard_normal((5, M * dsub)).astype(np.float32)
+    d, i = oracle.adc_search(oracle.adc_lut(Q, C), codes, 10)
+    Xh = oracle.pq_decode(codes, C).astype(np.float64)
+    ref = ((Q[:, None, :].astype(np.float64) - Xh[None]) ** 2).sum(-1)
+    np.testing.assert_allclose(d, np.take_along_axis(ref, i.astype(np.int64), 1), rtol=1e-5)
+    assert np.all(np.diff(d, axis=1) >= 0)

@@ -1,0 +1,532 @@
+// adc.hip — flat ADC (asymmetric distance) search over PQ codes on gfx950.
+//
+// GPU counterpart of FlatQuantizedIndex.search_with_scores
+// (/root/reference/src/haag_vq/methods/search/flat_quantized_index.py:45-76), which decodes
+// every code and ranks ||q - x_hat||^2; here the same quantity is assembled from per-query
+// lookup tables, sum_m ||q_m - c_{m,code_m}||^2 (canonical order in include/mivq.h):
+//   adc_lut_kernel     one block per (query, subspace), one lane per centroid.
+//   adc_scan_kernel    LUTs of QB queries live in LDS; each wavefront streams 64 code rows
+//                      per step (one row per lane, 16-B loads), sums M table entries per
+//                      (row, query) and keeps, per query, a wave-resident top-k (element e of
+//                      the sorted list in lane e%64, register e/64) that a ballot screens and
+//                      a shift-insert updates.  Exact (dist, id) order, so results are
+//                      deterministic and identical for any row partition.
+//   topk_merge_kernel  merges the per-wave partial lists (and, after the RCCL all-gather,
+//                      the per-shard lists) into the final sorted top-k.
+#include "mivq_common.h"
+
+namespace mivq {
+namespace {
+
+constexpr uint32_t kNoId = 0xFFFFFFFFu;
+
+__device__ __forceinline__ bool pair_less(float da, uint32_t ia, float db, uint32_t ib) {
+    return da < db || (da == db && ia < ib);
+}
+
+// L2: lut[q][m][k] = fmaf chain over t of (q_t - c_t)^2;  IP: -(fmaf chain of q_t * c_t)
+__global__ void adc_lut_kernel(const float* __restrict__ q, int64_t nq, int d, int M, int ksub, int dsub,
+                               const float* __restrict__ C, int metric, float* __restrict__ lut) {
+    const int64_t qm = blockIdx.x;
+    const int64_t qi = qm / M;
+    const int m = (int)(qm % M);
+    const float* qs = q + qi * d + (int64_t)m * dsub;
+    for (int k = threadIdx.x; k < ksub; k += blockDim.x) {
+        const float* c = C + ((int64_t)m * ksub + k) * dsub;
+        float acc = 0.0f;
+        if (metric == MIVQ_METRIC_L2) {
+            for (int t = 0; t < dsub; ++t) {
+                const float df = __fsub_rn(qs[t], c[t]);
+                acc = __builtin_fmaf(df, df, acc);
+            }
+        } else {
+            for (int t = 0; t < dsub; ++t) acc = __builtin_fmaf(qs[t], c[t], acc);
+            acc = -acc;
+        }
+        lut[(qi * M + m) * ksub + k] = acc;
+    }
+}
+
+// R = registers per lane of the wave-resident sorted list (k <= 64 * R).
+template <int R>
+struct WaveTopK {
+    float d[R];
+    uint32_t id[R];
+
+    __device__ void init() {
+#pragma unroll
+        for (int r = 0; r < R; ++r) { d[r] = INFINITY; id[r] = kNoId; }
+    }
+    // element k-1 (the current threshold); wave-uniform
+    __device__ void kth(int k, float& kd, uint32_t& ki) const {
+        const int r = (k - 1) >> 6, ln = (k - 1) & 63;
+        float vd = d[0];
+        uint32_t vi = id[0];
+#pragma unroll
+        for (int q = 1; q < R; ++q) if (q == r) { vd = d[q]; vi = id[q]; }
+        kd = __shfl(vd, ln);
+        ki = __shfl(vi, ln);
+    }
+    // insert (cd, ci) known to be < element k-1; wave-uniform call
+    __device__ void insert(float cd, uint32_t ci, int k, int lane) {
+        int p = 0;
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+            const int e = r * 64 + lane;
+            p += __popcll(__ballot(e < k && pair_less(d[r], id[r], cd, ci)));
+        }
+        float nd[R];
+        uint32_t ni[R];
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+            // element e-1: lane-1 of the same register, or lane 63 of register r-1
+            float pd = __shfl_up(d[r], 1);
+            uint32_t pi = __shfl_up(id[r], 1);
+            float td = INFINITY;
+            uint32_t ti = kNoId;
+            if (r > 0) {  // compile-time r: wave-uniform shuffle
+                td = __shfl(d[r > 0 ? r - 1 : 0], 63);
+                ti = __shfl(id[r > 0 ? r - 1 : 0], 63);
+            }
+            if (lane == 0) { pd = td; pi = ti; }
+            const int e = r * 64 + lane;
+            nd[r] = e > p ? pd : (e == p ? cd : d[r]);
+            ni[r] = e > p ? pi : (e == p ? ci : id[r]);
+        }
+#pragma unroll
+        for (int r = 0; r < R; ++r) { d[r] = nd[r]; id[r] = ni[r]; }
+    }
+};
+
+// grid (nchunks, ceil(nq / QB)), block 256 (4 waves).  Part index = chunk * 4 + wave.
+template <int R, int QB>
+__global__ __launch_bounds__(256) void adc_scan_kernel(
+    const float* __restrict__ lut, int64_t nq, const uint8_t* __restrict__ codes, int64_t n, int M,
+    int ksub, int k, int64_t id_offset, int64_t chunk_rows, float* __restrict__ part_d,
+    uint32_t* __restrict__ part_i) {
+    extern __shared__ __attribute__((aligned(16))) float tab[];  // [QB][M][ksub]
+    const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+    const int64_t q0 = (int64_t)blockIdx.y * QB;
+    const int nqb = (int)min<int64_t>(QB, nq - q0);
+    const int64_t tab_elems = (int64_t)M * ksub;
+    // stage the LUTs (16-B copies)
+    if ((tab_elems & 3) == 0) {
+        const float4* src = reinterpret_cast<const float4*>(lut + q0 * tab_elems);
+        float4* dst = reinterpret_cast<float4*>(tab);
+        const int64_t cnt = (int64_t)nqb * tab_elems / 4;
+        for (int64_t e = tid; e < cnt; e += 256) dst[e] = src[e];
+    } else {
+        const int64_t cnt = (int64_t)nqb * tab_elems;
+        for (int64_t e = tid; e < cnt; e += 256) tab[e] = lut[q0 * tab_elems + e];
+    }
+    __syncthreads();
+
+    WaveTopK<R> top[QB];
+#pragma unroll
+    for (int qq = 0; qq < QB; ++qq) top[qq].init();
+
+    const int64_t rbeg = (int64_t)blockIdx.x * chunk_rows;
+    const int64_t rend = min(n, rbeg + chunk_rows);
+    const bool words = (M % 4) == 0;
+    for (int64_t base = rbeg + (int64_t)wv * 64; base < rend; base += 256) {
+        const int64_t row = base + lane;
+        const bool valid = row < rend;
+        float dist[QB];
+#pragma unroll
+        for (int qq = 0; qq < QB; ++qq) dist[qq] = 0.0f;
+        if (valid) {
+            const uint8_t* cr = codes + row * M;
+            if (words) {
+                for (int m0 = 0; m0 < M; m0 += 4) {
+                    const uint32_t wrd = *reinterpret_cast<const uint32_t*>(cr + m0);
+#pragma unroll
+                    for (int b = 0; b < 4; ++b) {
+                        const uint32_t code = (wrd >> (8 * b)) & 0xFFu;
+                        const float* tcol = tab + (int64_t)(m0 + b) * ksub + code;
+#pragma unroll
+                        for (int qq = 0; qq < QB; ++qq) dist[qq] += tcol[qq * tab_elems];
+                    }
+                }
+            } else {
+                for (int m = 0; m < M; ++m) {
+                    const float* tcol = tab + (int64_t)m * ksub + cr[m];
+#pragma unroll
+                    for (int qq = 0; qq < QB; ++qq) dist[qq] += tcol[qq * tab_elems];
+                }
+            }
+        }
+        const uint32_t gid = (uint32_t)(id_offset + row);
+#pragma unroll
+        for (int qq = 0; qq < QB; ++qq) {
+            if (qq >= nqb) break;
+            float dv = dist[qq];
+            if (dv != dv) dv = INFINITY;  // NaN ranks with +inf
+            float kd;
+            uint32_t ki;
+            top[qq].kth(k, kd, ki);
+            unsigned long long mask = __ballot(valid && pair_less(dv, gid, kd, ki));
+            while (mask) {
+                const int src = __builtin_ctzll(mask);
+                mask &= mask - 1;
+                const float cd = __shfl(dv, src);
+                const uint32_t ci = __shfl(gid, src);
+                top[qq].kth(k, kd, ki);
+                if (!pair_less(cd, ci, kd, ki)) continue;
+                top[qq].insert(cd, ci, k, lane);
+            }
+        }
+    }
+    const int64_t part = (int64_t)blockIdx.x * 4 + wv;
+#pragma unroll
+    for (int qq = 0; qq < QB; ++qq) {
+        if (qq >= nqb) break;
+        float* od = part_d + (part * nq + q0 + qq) * k;
+        uint32_t* oi = part_i + (part * nq + q0 + qq) * k;
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+            const int e = r * 64 + lane;
+            if (e < k) { od[e] = top[qq].d[r]; oi[e] = top[qq].id[r]; }
+        }
+    }
+}
+
+// Exact brute force over an f32 database: grid (nchunks, ceil(nq / QB)), block 256.  The QB
+// query vectors live in LDS; lane = database row, distances are sequential fmaf chains over t
+// (16-B loads of the row), ranked with the same wave-resident top-k as adc_scan_kernel.
+template <int R, int QB>
+__global__ __launch_bounds__(256) void flat_scan_kernel(
+    const float* __restrict__ q, int64_t nq, const float* __restrict__ x, int64_t n, int d, int metric, int k,
+    int64_t id_offset, int64_t chunk_rows, float* __restrict__ part_d, uint32_t* __restrict__ part_i) {
+    extern __shared__ __attribute__((aligned(16))) float qv[];  // [QB][d]
+    const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+    const int64_t q0 = (int64_t)blockIdx.y * QB;
+    const int nqb = (int)min<int64_t>(QB, nq - q0);
+    for (int64_t e = tid; e < (int64_t)nqb * d; e += 256) qv[e] = q[q0 * d + e];
+    __syncthreads();
+    WaveTopK<R> top[QB];
+#pragma unroll
+    for (int qq = 0; qq < QB; ++qq) top[qq].init();
+    const int64_t rbeg = (int64_t)blockIdx.x * chunk_rows;
+    const int64_t rend = min(n, rbeg + chunk_rows);
+    const bool vec = (d % 4) == 0;
+    for (int64_t base = rbeg + (int64_t)wv * 64; base < rend; base += 256) {
+        const int64_t row = base + lane;
+        const bool valid = row < rend;
+        float dist[QB];
+#pragma unroll
+        for (int qq = 0; qq < QB; ++qq) dist[qq] = 0.0f;
+        if (valid) {
+            const float* xr = x + row * d;
+            if (vec) {
+                for (int t = 0; t < d; t += 4) {
+                    const float4 xv = *reinterpret_cast<const float4*>(xr + t);
+#pragma unroll
+                    for (int qq = 0; qq < QB; ++qq) {
+                        const float4 qf = *reinterpret_cast<const float4*>(qv + qq * d + t);
+                        if (metric == MIVQ_METRIC_L2) {
+                            float df = __fsub_rn(qf.x, xv.x); dist[qq] = __builtin_fmaf(df, df, dist[qq]);
+                            df = __fsub_rn(qf.y, xv.y); dist[qq] = __builtin_fmaf(df, df, dist[qq]);
+                            df = __fsub_rn(qf.z, xv.z); dist[qq] = __builtin_fmaf(df, df, dist[qq]);
+                            df = __fsub_rn(qf.w, xv.w); dist[qq] = __builtin_fmaf(df, df, dist[qq]);
+                        } else {
+                            dist[qq] = __builtin_fmaf(qf.x, xv.x, dist[qq]);
+                            dist[qq] = __builtin_fmaf(qf.y, xv.y, dist[qq]);
+                            dist[qq] = __builtin_fmaf(qf.z, xv.z, dist[qq]);
+                            dist[qq] = __builtin_fmaf(qf.w, xv.w, dist[qq]);
+                        }
+                    }
+                }
+            } else {
+                for (int t = 0; t < d; ++t) {
+                    const float xs = xr[t];
+#pragma unroll
+                    for (int qq = 0; qq < QB; ++qq) {
+                        if (metric == MIVQ_METRIC_L2) {
+                            const float df = __fsub_rn(qv[qq * d + t], xs);
+                            dist[qq] = __builtin_fmaf(df, df, dist[qq]);
+                        } else {
+                            dist[qq] = __builtin_fmaf(qv[qq * d + t], xs, dist[qq]);
+                        }
+                    }
+                }
+            }
+        }
+        const uint32_t gid = (uint32_t)(id_offset + row);
+#pragma unroll
+        for (int qq = 0; qq < QB; ++qq) {
+            if (qq >= nqb) break;
+            float dv = metric == MIVQ_METRIC_L2 ? dist[qq] : -dist[qq];
+            if (dv != dv) dv = INFINITY;
+            float kd;
+            uint32_t ki;
+            top[qq].kth(k, kd, ki);
+            unsigned long long mask = __ballot(valid && pair_less(dv, gid, kd, ki));
+            while (mask) {
+                const int src = __builtin_ctzll(mask);
+                mask &= mask - 1;
+                const float cd = __shfl(dv, src);
+                const uint32_t ci = __shfl(gid, src);
+                top[qq].kth(k, kd, ki);
+                if (!pair_less(cd, ci, kd, ki)) continue;
+                top[qq].insert(cd, ci, k, lane);
+            }
+        }
+    }
+    const int64_t part = (int64_t)blockIdx.x * 4 + wv;
+#pragma unroll
+    for (int qq = 0; qq < QB; ++qq) {
+        if (qq >= nqb) break;
+        float* od = part_d + (part * nq + q0 + qq) * k;
+        uint32_t* oi = part_i + (part * nq + q0 + qq) * k;
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+            const int e = r * 64 + lane;
+            if (e < k) { od[e] = top[qq].d[r]; oi[e] = top[qq].id[r]; }
+        }
+    }
+}
+
+// One thread per query: k-way selection over `parts` sorted lists laid out (parts, nq, k).
+__global__ void topk_merge_kernel(const float* __restrict__ in_d, const uint32_t* __restrict__ in_i,
+                                  int parts, int64_t nq, int k, float* __restrict__ out_d,
+                                  uint32_t* __restrict__ out_i) {
+    const int64_t qi = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (qi >= nq) return;
+    // cursor per part kept implicitly: count how many of each part were consumed in a
+    // small local array when parts is small, else fall back to a rescan.
+    constexpr int kMaxLocal = 64;
+    int cur_local[kMaxLocal];
+    const bool local = parts <= kMaxLocal;
+    if (local)
+        for (int p = 0; p < parts; ++p) cur_local[p] = 0;
+    float last_d = -INFINITY;
+    uint32_t last_i = 0;
+    bool have_last = false;
+    for (int j = 0; j < k; ++j) {
+        float bd = INFINITY;
+        uint32_t bi = kNoId;
+        int bp = -1;
+        for (int p = 0; p < parts; ++p) {
+            const float* ld = in_d + ((int64_t)p * nq + qi) * k;
+            const uint32_t* li = in_i + ((int64_t)p * nq + qi) * k;
+            int c;
+            if (local) {
+                c = cur_local[p];
+            } else {
+                // first element strictly after (last_d, last_i)
+                c = 0;
+                if (have_last)
+                    while (c < k && !pair_less(last_d, last_i, ld[c], li[c])) ++c;
+            }
+            if (c < k && (bp < 0 || pair_less(ld[c], li[c], bd, bi))) { bd = ld[c]; bi = li[c]; bp = p; }
+        }
+        if (bp >= 0 && local) cur_local[bp]++;
+        out_d[qi * k + j] = bp >= 0 ? bd : INFINITY;
+        out_i[qi * k + j] = bp >= 0 ? bi : kNoId;
+        last_d = bd; last_i = bi; have_last = true;
+    }
+}
+
+int adc_qb(int M, int ksub) {
+    const int64_t per = (int64_t)M * ksub * 4;
+    const int64_t budget = 128 * 1024;
+    if (per * 8 <= budget) return 8;
+    if (per * 4 <= budget) return 4;
+    if (per * 2 <= budget) return 2;
+    if (per <= 160 * 1024) return 1;
+    return 0;
+}
+
+int64_t adc_chunks(int64_t nq, int64_t n, int QB) {
+    const int64_t qblocks = ceil_div(nq, QB);
+    int64_t nch = ceil_div(2048, qblocks);
+    nch = std::max<int64_t>(1, std::min<int64_t>(nch, ceil_div(n, 1024)));
+    return nch;
+}
+
+template <int R, int QB>
+hipError_t launch_scan(const float* lut, int64_t nq, const uint8_t* codes, int64_t n, int M, int ksub, int k,
+                       int64_t id_offset, int64_t nch, float* pd, uint32_t* pi, hipStream_t st) {
+    const size_t smem = (size_t)QB * M * ksub * sizeof(float);
+    auto kern = adc_scan_kernel<R, QB>;
+    hipError_t e = hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);
+    if (e != hipSuccess) return e;
+    const int64_t chunk_rows = ceil_div(n, nch);
+    hipLaunchKernelGGL(kern, dim3((unsigned)nch, (unsigned)ceil_div(nq, QB)), dim3(256), smem, st, lut, nq, codes,
+                       n, M, ksub, k, id_offset, chunk_rows, pd, pi);
+    return hipGetLastError();
+}
+
+template <int R>
+hipError_t launch_scan_r(int QB, const float* lut, int64_t nq, const uint8_t* codes, int64_t n, int M, int ksub,
+                         int k, int64_t id_offset, int64_t nch, float* pd, uint32_t* pi, hipStream_t st) {
+    switch (QB) {
+        case 8: return launch_scan<R, 8>(lut, nq, codes, n, M, ksub, k, id_offset, nch, pd, pi, st);
+        case 4: return launch_scan<R, 4>(lut, nq, codes, n, M, ksub, k, id_offset, nch, pd, pi, st);
+        case 2: return launch_scan<R, 2>(lut, nq, codes, n, M, ksub, k, id_offset, nch, pd, pi, st);
+        default: return launch_scan<R, 1>(lut, nq, codes, n, M, ksub, k, id_offset, nch, pd, pi, st);
+    }
+}
+
+int flat_qb(int d) {
+    const int64_t per = (int64_t)d * 4;
+    if (per * 8 <= 96 * 1024) return 8;
+    if (per * 4 <= 96 * 1024) return 4;
+    if (per * 2 <= 96 * 1024) return 2;
+    if (per <= 160 * 1024) return 1;
+    return 0;
+}
+
+template <int R, int QB>
+hipError_t launch_flat(const float* q, int64_t nq, const float* x, int64_t n, int d, int metric, int k,
+                       int64_t id_offset, int64_t nch, float* pd, uint32_t* pi, hipStream_t st) {
+    const size_t smem = (size_t)QB * d * sizeof(float);
+    auto kern = flat_scan_kernel<R, QB>;
+    hipError_t e = hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(kern, dim3((unsigned)nch, (unsigned)ceil_div(nq, QB)), dim3(256), smem, st, q, nq, x, n, d,
+                       metric, k, id_offset, ceil_div(n, nch), pd, pi);
+    return hipGetLastError();
+}
+
+template <int R>
+hipError_t launch_flat_r(int QB, const float* q, int64_t nq, const float* x, int64_t n, int d, int metric, int k,
+                         int64_t id_offset, int64_t nch, float* pd, uint32_t* pi, hipStream_t st) {
+    switch (QB) {
+        case 8: return launch_flat<R, 8>(q, nq, x, n, d, metric, k, id_offset, nch, pd, pi, st);
+        case 4: return launch_flat<R, 4>(q, nq, x, n, d, metric, k, id_offset, nch, pd, pi, st);
+        case 2: return launch_flat<R, 2>(q, nq, x, n, d, metric, k, id_offset, nch, pd, pi, st);
+        default: return launch_flat<R, 1>(q, nq, x, n, d, metric, k, id_offset, nch, pd, pi, st);
+    }
+}
+
+}  // namespace
+}  // namespace mivq
+
+using namespace mivq;
+
+extern "C" size_t mivq_flat_search_workspace_bytes(int64_t nq, int64_t n, int32_t d, int32_t k) {
+    if (nq <= 0 || n <= 0 || d <= 0 || k <= 0) return 0;
+    const int QB = flat_qb(d);
+    if (QB == 0) return 0;
+    const int64_t parts = adc_chunks(nq, n, QB) * 4;
+    return align_up((size_t)parts * nq * k * sizeof(float), 256) + align_up((size_t)parts * nq * k * 4, 256);
+}
+
+extern "C" int mivq_flat_search(const float* q, int64_t nq, const float* x, int64_t n, int32_t d, int32_t metric,
+                                int32_t k, int64_t id_offset, void* workspace, size_t workspace_bytes, float* dists,
+                                uint32_t* ids, void* stream) {
+    MIVQ_REQUIRE(nq >= 0 && n >= 0 && d > 0 && k > 0, MIVQ_ERR_INVALID, "flat_search: bad sizes");
+    MIVQ_REQUIRE(k <= 256, MIVQ_ERR_UNSUPPORTED, "flat_search: k=%d > 256", k);
+    MIVQ_REQUIRE(metric == MIVQ_METRIC_L2 || metric == MIVQ_METRIC_INNER_PRODUCT, MIVQ_ERR_UNSUPPORTED,
+                 "flat_search: metric %d", metric);
+    const int QB = flat_qb(d);
+    MIVQ_REQUIRE(QB > 0, MIVQ_ERR_UNSUPPORTED, "flat_search: d=%d too large for LDS", d);
+    MIVQ_REQUIRE(id_offset >= 0 && id_offset + n <= (int64_t)kNoId, MIVQ_ERR_INVALID, "flat_search: ids overflow");
+    if (nq == 0) return MIVQ_OK;
+    hipStream_t st = as_stream(stream);
+    MIVQ_REQUIRE(dists && ids, MIVQ_ERR_INVALID, "flat_search: null pointer");
+    if (n == 0) {
+        hipLaunchKernelGGL(topk_merge_kernel, dim3((unsigned)ceil_div(nq, 256)), dim3(256), 0, st,
+                           (const float*)nullptr, (const uint32_t*)nullptr, 0, nq, k, dists, ids);
+        return check_launch("flat_search(empty)");
+    }
+    MIVQ_REQUIRE(q && x, MIVQ_ERR_INVALID, "flat_search: null pointer");
+    const size_t need = mivq_flat_search_workspace_bytes(nq, n, d, k);
+    MIVQ_REQUIRE(workspace && workspace_bytes >= need, MIVQ_ERR_WORKSPACE, "flat_search: workspace %zu < %zu",
+                 workspace_bytes, need);
+    const int64_t nch = adc_chunks(nq, n, QB);
+    const int parts = (int)(nch * 4);
+    float* pd = static_cast<float*>(workspace);
+    uint32_t* pi = reinterpret_cast<uint32_t*>(static_cast<unsigned char*>(workspace) +
+                                               align_up((size_t)parts * nq * k * sizeof(float), 256));
+    const int R = (k + 63) / 64;
+    hipError_t e;
+    switch (R) {
+        case 1: e = launch_flat_r<1>(QB, q, nq, x, n, d, metric, k, id_offset, nch, pd, pi, st); break;
+        case 2: e = launch_flat_r<2>(QB, q, nq, x, n, d, metric, k, id_offset, nch, pd, pi, st); break;
+        case 3: e = launch_flat_r<3>(QB, q, nq, x, n, d, metric, k, id_offset, nch, pd, pi, st); break;
+        default: e = launch_flat_r<4>(QB, q, nq, x, n, d, metric, k, id_offset, nch, pd, pi, st); break;
+    }
+    if (e != hipSuccess) return set_error(MIVQ_ERR_HIP, "flat_scan: %s", hipGetErrorString(e));
+    hipLaunchKernelGGL(topk_merge_kernel, dim3((unsigned)ceil_div(nq, 256)), dim3(256), 0, st, pd, pi, parts, nq, k,
+                       dists, ids);
+    return check_launch("topk_merge");
+}
+
+extern "C" int mivq_adc_lut(const float* q, int64_t nq, int32_t d, int32_t M, int32_t nbits,
+                            const float* centroids, int32_t metric, float* lut, void* stream) {
+    MIVQ_REQUIRE(metric == MIVQ_METRIC_L2 || metric == MIVQ_METRIC_INNER_PRODUCT, MIVQ_ERR_UNSUPPORTED,
+                 "adc_lut: metric %d", metric);
+    MIVQ_REQUIRE(nq >= 0 && M > 0 && d > 0 && d % M == 0, MIVQ_ERR_INVALID, "adc_lut: bad sizes");
+    MIVQ_REQUIRE(nbits >= 1 && nbits <= 8, MIVQ_ERR_UNSUPPORTED, "adc_lut: nbits=%d", nbits);
+    if (nq == 0) return MIVQ_OK;
+    MIVQ_REQUIRE(q && centroids && lut, MIVQ_ERR_INVALID, "adc_lut: null pointer");
+    const int ksub = 1 << nbits;
+    hipLaunchKernelGGL(adc_lut_kernel, dim3((unsigned)(nq * M)), dim3(ksub < 64 ? 64 : ksub), 0, as_stream(stream),
+                       q, nq, d, M, ksub, d / M, centroids, metric, lut);
+    return check_launch("adc_lut");
+}
+
+extern "C" size_t mivq_adc_search_workspace_bytes(int64_t nq, int64_t n, int32_t M, int32_t nbits, int32_t k) {
+    if (nq <= 0 || n <= 0 || M <= 0 || k <= 0 || nbits < 1 || nbits > 8) return 0;
+    const int QB = adc_qb(M, 1 << nbits);
+    if (QB == 0) return 0;
+    const int64_t parts = adc_chunks(nq, n, QB) * 4;
+    return align_up((size_t)parts * nq * k * sizeof(float), 256) + align_up((size_t)parts * nq * k * 4, 256);
+}
+
+extern "C" int mivq_adc_search(const float* lut, int64_t nq, const uint8_t* codes, int64_t n, int32_t M,
+                               int32_t nbits, int32_t k, int64_t id_offset, void* workspace,
+                               size_t workspace_bytes, float* dists, uint32_t* ids, void* stream) {
+    MIVQ_REQUIRE(nq >= 0 && n >= 0 && M > 0 && k > 0, MIVQ_ERR_INVALID,
+                 "adc_search: bad sizes nq=%lld n=%lld M=%d k=%d", (long long)nq, (long long)n, M, k);
+    MIVQ_REQUIRE(nbits >= 1 && nbits <= 8, MIVQ_ERR_UNSUPPORTED, "adc_search: nbits=%d", nbits);
+    MIVQ_REQUIRE(k <= 256, MIVQ_ERR_UNSUPPORTED, "adc_search: k=%d > 256", k);
+    const int ksub = 1 << nbits;
+    const int QB = adc_qb(M, ksub);
+    MIVQ_REQUIRE(QB > 0, MIVQ_ERR_UNSUPPORTED, "adc_search: M*ksub=%d tables do not fit LDS", M * ksub);
+    MIVQ_REQUIRE(id_offset >= 0 && id_offset + n <= (int64_t)kNoId, MIVQ_ERR_INVALID,
+                 "adc_search: global ids must fit uint32");
+    if (nq == 0) return MIVQ_OK;
+    hipStream_t st = as_stream(stream);
+    if (n == 0) {
+        // nothing to rank: every slot is the sentinel
+        MIVQ_REQUIRE(dists && ids, MIVQ_ERR_INVALID, "adc_search: null pointer");
+        hipLaunchKernelGGL(topk_merge_kernel, dim3((unsigned)ceil_div(nq, 256)), dim3(256), 0, st,
+                           (const float*)nullptr, (const uint32_t*)nullptr, 0, nq, k, dists, ids);
+        return check_launch("adc_search(empty)");
+    }
+    MIVQ_REQUIRE(lut && codes && dists && ids, MIVQ_ERR_INVALID, "adc_search: null pointer");
+    const size_t need = mivq_adc_search_workspace_bytes(nq, n, M, nbits, k);
+    MIVQ_REQUIRE(workspace && workspace_bytes >= need, MIVQ_ERR_WORKSPACE, "adc_search: workspace %zu < %zu",
+                 workspace_bytes, need);
+    const int64_t nch = adc_chunks(nq, n, QB);
+    const int parts = (int)(nch * 4);
+    float* pd = static_cast<float*>(workspace);
+    uint32_t* pi = reinterpret_cast<uint32_t*>(static_cast<unsigned char*>(workspace) +
+                                               align_up((size_t)parts * nq * k * sizeof(float), 256));
+    const int R = (k + 63) / 64;
+    hipError_t e;
+    switch (R) {
+        case 1: e = launch_scan_r<1>(QB, lut, nq, codes, n, M, ksub, k, id_offset, nch, pd, pi, st); break;
+        case 2: e = launch_scan_r<2>(QB, lut, nq, codes, n, M, ksub, k, id_offset, nch, pd, pi, st); break;
+        case 3: e = launch_scan_r<3>(QB, lut, nq, codes, n, M, ksub, k, id_offset, nch, pd, pi, st); break;
+        default: e = launch_scan_r<4>(QB, lut, nq, codes, n, M, ksub, k, id_offset, nch, pd, pi, st); break;
+    }
+    if (e != hipSuccess) return set_error(MIVQ_ERR_HIP, "adc_scan: %s", hipGetErrorString(e));
+    hipLaunchKernelGGL(topk_merge_kernel, dim3((unsigned)ceil_div(nq, 256)), dim3(256), 0, st, pd, pi, parts, nq, k,
+                       dists, ids);
+    return check_launch("topk_merge");
+}
+
+extern "C" int mivq_topk_merge(const float* dists_in, const uint32_t* ids_in, int32_t parts, int64_t nq, int32_t k,
+                               float* dists_out, uint32_t* ids_out, void* stream) {
+    MIVQ_REQUIRE(parts >= 0 && nq >= 0 && k > 0, MIVQ_ERR_INVALID, "topk_merge: bad sizes");
+    if (nq == 0) return MIVQ_OK;
+    MIVQ_REQUIRE((parts == 0 || (dists_in && ids_in)) && dists_out && ids_out, MIVQ_ERR_INVALID,
+                 "topk_merge: null pointer");
+    hipLaunchKernelGGL(topk_merge_kernel, dim3((unsigned)ceil_div(nq, 256)), dim3(256), 0, as_stream(stream),
+                       dists_in, ids_in, parts, nq, k, dists_out, ids_out);
+    return check_launch("topk_merge");
+}

@@ -1,0 +1,369 @@
+"""ctypes binding of libmivq.so — the MI355X HIP implementation of the hot path.
+
+Every public function here takes torch tensors that already live on the current HIP
+device, validates shape / dtype / contiguity on the host, and calls the matching C entry
+point of ``include/mivq.h`` on the current torch stream.  There is no CPU fallback: on a
+machine without a HIP device (or without the built library) every compute call raises.
+
+The error mapping mirrors the reference's exceptions:
+  MIVQ_ERR_INVALID     -> ValueError (AssertionError for "D must be divisible by M",
+                          product_quantization.py:61-62)
+  MIVQ_ERR_UNSUPPORTED -> ValueError
+  MIVQ_ERR_HIP / _WORKSPACE -> RuntimeError
+"""
+
+from __future__ import annotations
+
+import ctypes
+import os
+import threading
+from pathlib import Path
+from typing import Optional, Tuple
+
+import torch  # noqa: F401  (must be imported before libmivq: they share libamdhip64.so.7)
+
+_PKG_ROOT = Path(__file__).resolve().parent.parent  # vector-quantization_amd/
+LIB_PATH = Path(os.environ.get("MIVQ_LIB", _PKG_ROOT / "lib" / "libmivq.so"))
+
+MIVQ_OK = 0
+MIVQ_ERR_INVALID = -1
+MIVQ_ERR_UNSUPPORTED = -2
+MIVQ_ERR_HIP = -3
+MIVQ_ERR_WORKSPACE = -4
+MIVQ_PQ_AUTO = 0
+MIVQ_PQ_FORCE_EXACT = 1
+METRIC_INNER_PRODUCT = 0
+METRIC_L2 = 1
+NO_ID = 0xFFFFFFFF
+
+_c = ctypes
+_vp, _i32, _i64, _u32, _sz = _c.c_void_p, _c.c_int32, _c.c_int64, _c.c_uint32, _c.c_size_t
+
+# name -> (restype, argtypes); exactly the declarations of include/mivq.h
+SIGNATURES = {
+    "mivq_last_error": (_c.c_char_p, []),
+    "mivq_abi_version": (_c.c_int, []),
+    "mivq_device_info": (_c.c_int, [_c.c_int, _c.c_char_p, _c.POINTER(_i32), _c.POINTER(_i64), _c.POINTER(_i64)]),
+    "mivq_pq_prep_bytes": (_sz, [_i32, _i32, _i32]),
+    "mivq_pq_prepare": (_c.c_int, [_vp, _i32, _i32, _i32, _vp, _vp]),
+    "mivq_pq_encode_workspace_bytes": (_sz, [_i64, _i32, _i32, _i32]),
+    "mivq_pq_encode": (_c.c_int, [_vp, _i64, _i32, _i32, _i32, _vp, _vp, _vp, _sz, _vp, _u32, _vp]),
+    "mivq_pq_decode": (_c.c_int, [_vp, _i64, _i32, _i32, _i32, _vp, _vp, _vp]),
+    "mivq_pq_unpack": (_c.c_int, [_vp, _i64, _i32, _i32, _vp, _vp]),
+    "mivq_kmeans_update": (_c.c_int, [_vp, _i64, _i32, _i32, _i32, _vp, _vp, _vp, _vp]),
+    "mivq_opq_rotate": (_c.c_int, [_vp, _i64, _i32, _vp, _i32, _vp, _vp]),
+    "mivq_sq_encode_f32": (_c.c_int, [_vp, _i64, _i32, _vp, _vp, _i32, _vp, _vp]),
+    "mivq_sq_encode_f64": (_c.c_int, [_vp, _i64, _i32, _vp, _vp, _i32, _vp, _vp]),
+    "mivq_sq_decode_f32": (_c.c_int, [_vp, _i64, _i32, _vp, _vp, _i32, _vp, _vp]),
+    "mivq_sq_decode_f64": (_c.c_int, [_vp, _i64, _i32, _vp, _vp, _i32, _vp, _vp]),
+    "mivq_rabitq_encode": (_c.c_int, [_vp, _i64, _i32, _vp, _i32, _vp, _vp]),
+    "mivq_rabitq_decode": (_c.c_int, [_vp, _i64, _i32, _vp, _vp, _vp]),
+    "mivq_adc_lut": (_c.c_int, [_vp, _i64, _i32, _i32, _i32, _vp, _i32, _vp, _vp]),
+    "mivq_adc_search_workspace_bytes": (_sz, [_i64, _i64, _i32, _i32, _i32]),
+    "mivq_adc_search": (_c.c_int, [_vp, _i64, _vp, _i64, _i32, _i32, _i32, _i64, _vp, _sz, _vp, _vp, _vp]),
+    "mivq_flat_search_workspace_bytes": (_sz, [_i64, _i64, _i32, _i32]),
+    "mivq_flat_search": (_c.c_int, [_vp, _i64, _vp, _i64, _i32, _i32, _i32, _i64, _vp, _sz, _vp, _vp, _vp]),
+    "mivq_topk_merge": (_c.c_int, [_vp, _vp, _i32, _i64, _i32, _vp, _vp, _vp]),
+}
+
+_lib: Optional[ctypes.CDLL] = None
+_lock = threading.Lock()
+
+
+def load_library() -> ctypes.CDLL:
+    """Load libmivq.so and bind every exported symbol (works without a GPU)."""
+    global _lib
+    with _lock:
+        if _lib is None:
+            if not LIB_PATH.exists():
+                raise RuntimeError(
+                    f"libmivq.so not found at {LIB_PATH}; build it with "
+                    "`make -C vector-quantization_amd/csrc` (or __graft_entry__.build())"
+                )
+            lib = ctypes.CDLL(str(LIB_PATH))
+            for name, (res, args) in SIGNATURES.items():
+                fn = getattr(lib, name)
+                fn.restype = res
+                fn.argtypes = args
+            _lib = lib
+    return _lib
+
+
+def require_device() -> torch.device:
+    """The HIP device compute runs on; raises when none is visible (no CPU fallback)."""
+    if not torch.cuda.is_available():
+        raise RuntimeError(
+            "haag_vq (MI355X build) needs a HIP device: no GPU is visible and this "
+            "implementation has no CPU fallback"
+        )
+    load_library()
+    return torch.device("cuda", torch.cuda.current_device())
+
+
+def _raise(rc: int) -> None:
+    msg = load_library().mivq_last_error().decode(errors="replace")
+    if rc == MIVQ_ERR_INVALID:
+        if "divisible" in msg:
+            raise AssertionError(msg)
+        raise ValueError(msg)
+    if rc == MIVQ_ERR_UNSUPPORTED:
+        raise ValueError(msg)
+    raise RuntimeError(msg)
+
+
+def _call(name: str, *args) -> None:
+    rc = getattr(load_library(), name)(*args)
+    if rc != MIVQ_OK:
+        _raise(rc)
+
+
+def _stream() -> ctypes.c_void_p:
+    return ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+
+
+def _ptr(t: Optional[torch.Tensor]):
+    return None if t is None else ctypes.c_void_p(t.data_ptr())
+
+
+def _check(t: torch.Tensor, name: str, dtype: torch.dtype, ndim: Optional[int] = None) -> None:
+    if not isinstance(t, torch.Tensor):
+        raise TypeError(f"{name}: expected a torch.Tensor")
+    if not t.is_cuda:
+        raise ValueError(f"{name}: tensor must live on the HIP device")
+    if t.dtype != dtype:
+        raise ValueError(f"{name}: dtype {t.dtype} != {dtype}")
+    if ndim is not None and t.dim() != ndim:
+        raise ValueError(f"{name}: expected {ndim}-D, got shape {tuple(t.shape)}")
+    if not t.is_contiguous():
+        raise ValueError(f"{name}: tensor must be contiguous")
+
+
+# ----------------------------------------------------------------- workspace
+_ws: dict = {}
+
+
+def workspace(nbytes: int, device: torch.device) -> torch.Tensor:
+    """Grow-only per-(device, stream) scratch buffer (the library never allocates)."""
+    key = (device.index, torch.cuda.current_stream(device).cuda_stream)
+    buf = _ws.get(key)
+    if buf is None or buf.numel() < nbytes:
+        buf = torch.empty(max(int(nbytes), 256), dtype=torch.uint8, device=device)
+        _ws[key] = buf
+    return buf
+
+
+# ----------------------------------------------------------------- device info
+def device_info(device: int = 0) -> dict:
+    name = ctypes.create_string_buffer(64)
+    cus, lds, hbm = _i32(), _i64(), _i64()
+    _call("mivq_device_info", device, name, ctypes.byref(cus), ctypes.byref(lds), ctypes.byref(hbm))
+    return {"arch": name.value.decode(), "cus": cus.value, "lds_per_cu": lds.value, "hbm_bytes": hbm.value}
+
+
+# ----------------------------------------------------------------- PQ
+def pq_code_size(M: int, nbits: int) -> int:
+    return (M * nbits + 7) // 8
+
+
+def pq_prepare(centroids: torch.Tensor, nbits: int) -> torch.Tensor:
+    """centroids (M, ksub, dsub) f32 -> prep bytes for pq_encode."""
+    _check(centroids, "centroids", torch.float32, 3)
+    M, ksub, dsub = centroids.shape
+    if ksub != (1 << nbits):
+        raise ValueError(f"centroids have ksub={ksub}, expected 2**{nbits}")
+    d = M * dsub
+    nb = load_library().mivq_pq_prep_bytes(d, M, nbits)
+    prep = torch.empty(nb, dtype=torch.uint8, device=centroids.device)
+    _call("mivq_pq_prepare", _ptr(centroids), d, M, nbits, _ptr(prep), _stream())
+    return prep
+
+
+def pq_encode(x: torch.Tensor, centroids: torch.Tensor, prep: torch.Tensor, nbits: int,
+              exact: bool = False, out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    _check(x, "x", torch.float32, 2)
+    _check(centroids, "centroids", torch.float32, 3)
+    n, d = x.shape
+    M, ksub, dsub = centroids.shape
+    if d != M * dsub:
+        raise ValueError(f"x has d={d}, codebook expects {M * dsub}")
+    cs = pq_code_size(M, nbits)
+    if out is None:
+        out = torch.empty((n, cs), dtype=torch.uint8, device=x.device)
+    else:
+        _check(out, "out", torch.uint8, 2)
+        if tuple(out.shape) != (n, cs):
+            raise ValueError(f"out shape {tuple(out.shape)} != {(n, cs)}")
+    nb = load_library().mivq_pq_encode_workspace_bytes(n, d, M, nbits)
+    ws = workspace(nb, x.device)
+    flags = MIVQ_PQ_FORCE_EXACT if exact else MIVQ_PQ_AUTO
+    _call("mivq_pq_encode", _ptr(x), n, d, M, nbits, _ptr(centroids), _ptr(prep), _ptr(ws), ws.numel(),
+          _ptr(out), flags, _stream())
+    return out
+
+
+def pq_decode(codes: torch.Tensor, centroids: torch.Tensor, nbits: int,
+              out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    _check(codes, "codes", torch.uint8, 2)
+    _check(centroids, "centroids", torch.float32, 3)
+    M, ksub, dsub = centroids.shape
+    n = codes.shape[0]
+    if codes.shape[1] != pq_code_size(M, nbits):
+        raise ValueError(f"codes have {codes.shape[1]} bytes per row, expected {pq_code_size(M, nbits)}")
+    d = M * dsub
+    if out is None:
+        out = torch.empty((n, d), dtype=torch.float32, device=codes.device)
+    _call("mivq_pq_decode", _ptr(codes), n, d, M, nbits, _ptr(centroids), _ptr(out), _stream())
+    return out
+
+
+def pq_unpack(codes: torch.Tensor, M: int, nbits: int) -> torch.Tensor:
+    _check(codes, "codes", torch.uint8, 2)
+    n = codes.shape[0]
+    out = torch.empty((n, M), dtype=torch.uint8, device=codes.device)
+    _call("mivq_pq_unpack", _ptr(codes), n, M, nbits, _ptr(out), _stream())
+    return out
+
+
+def kmeans_update(x: torch.Tensor, assign: torch.Tensor, centroids: torch.Tensor,
+                  counts: torch.Tensor) -> None:
+    _check(x, "x", torch.float32, 2)
+    _check(assign, "assign", torch.uint8, 2)
+    _check(centroids, "centroids", torch.float32, 3)
+    _check(counts, "counts", torch.int32, 2)
+    n, d = x.shape
+    M, ksub, dsub = centroids.shape
+    _call("mivq_kmeans_update", _ptr(x), n, d, M, ksub, _ptr(assign), _ptr(centroids), _ptr(counts), _stream())
+
+
+# ----------------------------------------------------------------- OPQ
+def opq_rotate(x: torch.Tensor, A: torch.Tensor, transpose: bool = False,
+               out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    _check(x, "x", torch.float32, 2)
+    _check(A, "A", torch.float32, 2)
+    n, d = x.shape
+    if tuple(A.shape) != (d, d):
+        raise ValueError(f"A must be ({d}, {d}), got {tuple(A.shape)}")
+    if out is None:
+        out = torch.empty_like(x)
+    _call("mivq_opq_rotate", _ptr(x), n, d, _ptr(A), 1 if transpose else 0, _ptr(out), _stream())
+    return out
+
+
+# ----------------------------------------------------------------- SQ
+def sq_encode(x: torch.Tensor, lo: torch.Tensor, den: torch.Tensor, nbits: int) -> torch.Tensor:
+    if x.dtype not in (torch.float32, torch.float64):
+        raise ValueError(f"sq_encode: unsupported dtype {x.dtype}")
+    _check(x, "x", x.dtype, 2)
+    _check(lo, "lo", x.dtype, 1)
+    _check(den, "den", x.dtype, 1)
+    n, d = x.shape
+    if nbits == 16:
+        out = torch.empty((n, d), dtype=torch.int16, device=x.device)
+    elif nbits == 8:
+        out = torch.empty((n, d), dtype=torch.uint8, device=x.device)
+    elif nbits == 4:
+        out = torch.empty((n, (d + 1) // 2), dtype=torch.uint8, device=x.device)
+    else:
+        raise ValueError(f"num_bits must be 4, 8, or 16, got {nbits}")
+    fn = "mivq_sq_encode_f64" if x.dtype == torch.float64 else "mivq_sq_encode_f32"
+    _call(fn, _ptr(x), n, d, _ptr(lo), _ptr(den), nbits, _ptr(out), _stream())
+    return out
+
+
+def sq_decode(codes: torch.Tensor, d: int, lo: torch.Tensor, den: torch.Tensor, nbits: int) -> torch.Tensor:
+    if not codes.is_contiguous() or not codes.is_cuda:
+        raise ValueError("codes must be a contiguous device tensor")
+    n = codes.shape[0]
+    dt = lo.dtype
+    _check(lo, "lo", dt, 1)
+    _check(den, "den", dt, 1)
+    out = torch.empty((n, d), dtype=dt, device=codes.device)
+    fn = "mivq_sq_decode_f64" if dt == torch.float64 else "mivq_sq_decode_f32"
+    _call(fn, _ptr(codes), n, d, _ptr(lo), _ptr(den), nbits, _ptr(out), _stream())
+    return out
+
+
+# ----------------------------------------------------------------- RaBitQ
+def rabitq_code_size(d: int) -> int:
+    return (d + 7) // 8 + 8
+
+
+def rabitq_encode(x: torch.Tensor, centroid: Optional[torch.Tensor], metric: int) -> torch.Tensor:
+    _check(x, "x", torch.float32, 2)
+    if centroid is not None:
+        _check(centroid, "centroid", torch.float32, 1)
+    n, d = x.shape
+    out = torch.empty((n, rabitq_code_size(d)), dtype=torch.uint8, device=x.device)
+    _call("mivq_rabitq_encode", _ptr(x), n, d, _ptr(centroid), metric, _ptr(out), _stream())
+    return out
+
+
+def rabitq_decode(codes: torch.Tensor, d: int, centroid: Optional[torch.Tensor]) -> torch.Tensor:
+    _check(codes, "codes", torch.uint8, 2)
+    if codes.shape[1] != rabitq_code_size(d):
+        raise ValueError(f"codes have {codes.shape[1]} bytes per row, expected {rabitq_code_size(d)}")
+    n = codes.shape[0]
+    out = torch.empty((n, d), dtype=torch.float32, device=codes.device)
+    _call("mivq_rabitq_decode", _ptr(codes), n, d, _ptr(centroid), _ptr(out), _stream())
+    return out
+
+
+# ----------------------------------------------------------------- ADC / flat search
+def adc_lut(q: torch.Tensor, centroids: torch.Tensor, nbits: int, metric: int = METRIC_L2) -> torch.Tensor:
+    _check(q, "q", torch.float32, 2)
+    _check(centroids, "centroids", torch.float32, 3)
+    nq, d = q.shape
+    M, ksub, dsub = centroids.shape
+    if d != M * dsub:
+        raise ValueError(f"queries have d={d}, codebook expects {M * dsub}")
+    lut = torch.empty((nq, M, ksub), dtype=torch.float32, device=q.device)
+    _call("mivq_adc_lut", _ptr(q), nq, d, M, nbits, _ptr(centroids), metric, _ptr(lut), _stream())
+    return lut
+
+
+def adc_search(lut: torch.Tensor, codes_u8: torch.Tensor, k: int, nbits: int,
+               id_offset: int = 0) -> Tuple[torch.Tensor, torch.Tensor]:
+    """Returns (dists f32 (nq, k), ids int32 (nq, k) holding uint32 bit patterns)."""
+    _check(lut, "lut", torch.float32, 3)
+    _check(codes_u8, "codes", torch.uint8, 2)
+    nq, M, ksub = lut.shape
+    n = codes_u8.shape[0]
+    if codes_u8.shape[1] != M:
+        raise ValueError(f"codes have {codes_u8.shape[1]} sub-codes, LUT has M={M}")
+    dists = torch.empty((nq, k), dtype=torch.float32, device=lut.device)
+    ids = torch.empty((nq, k), dtype=torch.int32, device=lut.device)
+    nb = load_library().mivq_adc_search_workspace_bytes(nq, n, M, nbits, k)
+    ws = workspace(nb, lut.device)
+    _call("mivq_adc_search", _ptr(lut), nq, _ptr(codes_u8), n, M, nbits, k, id_offset, _ptr(ws), ws.numel(),
+          _ptr(dists), _ptr(ids), _stream())
+    return dists, ids
+
+
+def flat_search(q: torch.Tensor, x: torch.Tensor, k: int, metric: int = METRIC_L2,
+                id_offset: int = 0) -> Tuple[torch.Tensor, torch.Tensor]:
+    _check(q, "q", torch.float32, 2)
+    _check(x, "x", torch.float32, 2)
+    nq, d = q.shape
+    n = x.shape[0]
+    if x.shape[1] != d:
+        raise ValueError(f"database has d={x.shape[1]}, queries d={d}")
+    dists = torch.empty((nq, k), dtype=torch.float32, device=q.device)
+    ids = torch.empty((nq, k), dtype=torch.int32, device=q.device)
+    nb = load_library().mivq_flat_search_workspace_bytes(nq, n, d, k)
+    ws = workspace(nb, q.device)
+    _call("mivq_flat_search", _ptr(q), nq, _ptr(x), n, d, metric, k, id_offset, _ptr(ws), ws.numel(),
+          _ptr(dists), _ptr(ids), _stream())
+    return dists, ids
+
+
+def topk_merge(dists: torch.Tensor, ids: torch.Tensor, k: int) -> Tuple[torch.Tensor, torch.Tensor]:
+    """(parts, nq, k) sorted lists -> (nq, k) sorted list, same (dist, id) order."""
+    _check(dists, "dists", torch.float32, 3)
+    _check(ids, "ids", torch.int32, 3)
+    parts, nq, kk = dists.shape
+    if kk != k:
+        raise ValueError("list length != k")
+    od = torch.empty((nq, k), dtype=torch.float32, device=dists.device)
+    oi = torch.empty((nq, k), dtype=torch.int32, device=dists.device)
+    _call("mivq_topk_merge", _ptr(dists), _ptr(ids), parts, nq, k, _ptr(od), _ptr(oi), _stream())
+    return od, oi

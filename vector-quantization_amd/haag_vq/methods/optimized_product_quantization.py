@@ -1,0 +1,142 @@
+"""Optimized product quantization (OPQ) on the MI355X.
+
+Drop-in for the reference's ``OptimizedProductQuantizer``
+(/root/reference/src/haag_vq/methods/optimized_product_quantization.py:7-46), which wraps
+``faiss.OPQMatrix(D, M, D)`` + ``faiss.ProductQuantizer``:
+
+* fit: learn an orthonormal rotation A by the OPQ alternating optimisation faiss'
+  OPQMatrix documents (random orthonormal init from seed 1234, ``niter`` rounds of
+  {rotate the <= 65536-row training sample, train PQ (40 k-means iterations the first
+  round, 4 warm-started ones after), encode+decode, orthogonal-Procrustes update of A}),
+  then train a fresh PQ on the rotated data (:26-28).
+* compress = PQ encode of x . A^T (:31); decompress = PQ decode . A (:34).
+
+Hot path on device: the rotation is ``mivq_opq_rotate`` (exact-f32 MFMA GEMM), encode /
+decode are the PQ kernels.  The Procrustes step of training (a D x D product and SVD) uses
+the vendor libraries through torch — it is training, not the encode path.
+"""
+
+from __future__ import annotations
+
+import numpy as np
+import torch
+
+from .. import _arrays, _native
+from ._kmeans import train_pq
+from .base_quantizer import BaseQuantizer
+from .product_quantization import ProductQuantizer
+
+
+class OPQHandle:
+    """Stands where the reference keeps ``faiss.OPQMatrix`` (``model.opq``)."""
+
+    def __init__(self, A: torch.Tensor) -> None:
+        self.A_device = A
+        self.d_in = self.d_out = int(A.shape[0])
+        self.is_orthonormal = True
+
+    @property
+    def A(self) -> np.ndarray:
+        return _arrays.to_host(self.A_device).reshape(-1)
+
+    def _run(self, x, transpose: bool):
+        if _arrays.is_tensor(x):
+            return _native.opq_rotate(_arrays.to_device(x), self.A_device, transpose)
+        x = np.asarray(x, dtype=np.float32)
+        out = np.empty_like(x)
+        for s, e in _arrays.row_chunks(x.shape[0], x.shape[1] * 8):
+            out[s:e] = _arrays.to_host(_native.opq_rotate(_arrays.to_device(x[s:e]), self.A_device, transpose))
+        return out
+
+    def apply(self, x):
+        """y = x . A^T (faiss LinearTransform::apply)."""
+        return self._run(x, False)
+
+    def reverse_transform(self, y):
+        """x = y . A (inverse of an orthonormal A)."""
+        return self._run(y, True)
+
+
+class OptimizedProductQuantizer(BaseQuantizer):
+    def __init__(self, M: int, B: int = 8):
+        """OPQ (Ge et al., TPAMI 2013).  M sub-quantizers of 2**B centroids."""
+        self.M = M
+        self.B = B
+        self.opq: OPQHandle | None = None
+        self.pq = None
+        self._inner: ProductQuantizer | None = None
+        # OPQMatrix training parameters (faiss defaults)
+        self.niter = 50
+        self.niter_pq = 4
+        self.niter_pq_0 = 40
+        self.max_train_points = 256 * 256
+        self.seed = 1234
+
+    def _train_rotation(self, X: torch.Tensor) -> torch.Tensor:
+        n, d = X.shape
+        rng = np.random.default_rng(self.seed)
+        if n > self.max_train_points:
+            sel = np.sort(rng.permutation(n)[: self.max_train_points])
+            X = X[torch.from_numpy(sel).to(X.device)].contiguous()
+        Q, _ = np.linalg.qr(np.random.default_rng(self.seed).standard_normal((d, d)))
+        A = torch.from_numpy(Q.astype(np.float32)).to(X.device).contiguous()
+        C = None
+        for it in range(self.niter):
+            Y = _native.opq_rotate(X, A, False)
+            C = train_pq(Y, self.M, self.B, niter=self.niter_pq_0 if it == 0 else self.niter_pq,
+                         seed=self.seed, max_points_per_centroid=1000, init=C)
+            prep = _native.pq_prepare(C, self.B)
+            Yhat = _native.pq_decode(_native.pq_encode(Y, C, prep, self.B), C, self.B)
+            # orthogonal Procrustes: argmin_R ||X R^T - Yhat||  ->  R = V U^T, X^T Yhat = U S V^T
+            G = (X.double().T @ Yhat.double())
+            U, _, Vh = torch.linalg.svd(G)
+            A = (Vh.T @ U.T).float().contiguous()
+        return A
+
+    def fit(self, X) -> None:
+        Xd = _arrays.to_device(X, torch.float32)
+        N, D = Xd.shape
+        assert D % self.M == 0, "D must be divisible by M"
+        A = self._train_rotation(Xd)
+        self.opq = OPQHandle(A)
+        inner = ProductQuantizer(M=self.M, B=self.B)
+        inner.fit(_native.opq_rotate(Xd, A, False))
+        self._inner = inner
+        self.pq = inner.pq
+
+    def _require(self, what: str) -> None:
+        if self._inner is None or self.opq is None:
+            raise RuntimeError(f"OptimizedProductQuantizer must be fitted before {what}().")
+
+    def compress(self, X):
+        self._require("compress")
+        if _arrays.is_tensor(X):
+            return self._inner.compress(self.opq.apply(X))
+        X = np.asarray(X, dtype=np.float32)
+        out = np.empty((X.shape[0], _native.pq_code_size(self.M, self.B)), dtype=np.uint8)
+        for s, e in _arrays.row_chunks(X.shape[0], X.shape[1] * 8):
+            y = _native.opq_rotate(_arrays.to_device(X[s:e]), self.opq.A_device, False)
+            out[s:e] = _arrays.to_host(self._inner.compress(y))
+        return out
+
+    def decompress(self, compressed):
+        self._require("decompress")
+        if _arrays.is_tensor(compressed):
+            return self.opq.reverse_transform(self._inner.decompress(compressed))
+        compressed = np.asarray(compressed)
+        D = self.M * self._inner.chunk_dim
+        out = np.empty((compressed.shape[0], D), dtype=np.float32)
+        for s, e in _arrays.row_chunks(compressed.shape[0], D * 8):
+            c = _arrays.to_device(compressed[s:e], torch.uint8)
+            out[s:e] = _arrays.to_host(self.opq.reverse_transform(self._inner.decompress(c)))
+        return out
+
+    @property
+    def inner(self) -> ProductQuantizer:
+        self._require("inner")
+        return self._inner
+
+    def get_compression_ratio(self, X) -> float:
+        """D*4 / ceil(M*B/8) — optimized_product_quantization.py:36-46."""
+        D = int(X.shape[1])
+        return float(D * 4 / int((self.M * self.B + 7) // 8))

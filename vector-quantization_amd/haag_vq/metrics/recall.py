@@ -1,0 +1,35 @@
+"""Recall@k — /root/reference/src/haag_vq/metrics/recall.py:6-43.
+
+``evaluate_recall`` re-encodes the database (as the reference does) and ranks it for the
+first ``num_queries`` queries on the MI355X (ADC for PQ / OPQ, decode + exact search
+otherwise; see methods/search/flat_quantized_index.py) instead of a full numpy argsort.
+"""
+
+import numpy as np
+
+from haag_vq.methods.search.flat_quantized_index import ids_to_numpy, search_codes
+
+
+def retrieve(data, model, k: int, num_queries: int = 100) -> np.ndarray:
+    queries = np.asarray(data.queries[:num_queries], dtype=np.float32)
+    codes = model.compress(np.asarray(data.vectors, dtype=np.float32))
+    k = min(k, len(data.vectors))
+    _, ids = search_codes(model, codes, queries, k, "l2")
+    return ids_to_numpy(ids).astype(np.int64)
+
+
+def evaluate_recall(data, model, num_queries=100):
+    true_nn = data.ground_truth[:num_queries]
+    retrieved = retrieve(data, model, k=100, num_queries=num_queries)
+    return {
+        "recall@10": recall_at_k(true_nn, retrieved, k=10),
+        "recall@100": recall_at_k(true_nn, retrieved, k=100),
+    }
+
+
+def recall_at_k(true_nn: np.ndarray, retrieved: np.ndarray, k: int) -> float:
+    """Mean over queries of |gt[:k] & retrieved[:k]| / k."""
+    hits = 0
+    for i in range(len(true_nn)):
+        hits += len(set(np.asarray(true_nn[i, :k]).tolist()) & set(np.asarray(retrieved[i, :k]).tolist())) / k
+    return hits / len(true_nn)

@@ -57,13 +57,34 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-adc", action="store_true")
     ap.add_argument("--exact", action="store_true", help="force the exact VALU encode path")
+    ap.add_argument("--legacy", action="store_true", help="diagnostic: subspace-looping MFMA kernel")
+    ap.add_argument("--data", choices=("clustered", "gaussian"), default="clustered")
     return ap.parse_args()
 
 
-def synth(n, d, seed, dev):
+def synth(n, d, seed, dev, kind="clustered", centers_seed=12345, n_centers=4096, spread=0.02):
+    """Synthetic embedding-like rows, generated on the device.
+
+    gaussian : isotropic N(0, I) rows, L2-normalised (no neighbourhood structure: recall@k of
+               any quantizer is ~0 on it, and it is the worst case for the encode filter).
+    clustered: normalise(center[j] + spread * N(0, I)) with 4096 shared unit centers (seeded
+               identically on every rank) — neighbourhoods like real text embeddings.
+    """
     g = torch.Generator(device=dev)
     g.manual_seed(seed)
-    X = torch.randn((n, d), generator=g, device=dev, dtype=torch.float32)
+    if kind == "gaussian":
+        X = torch.randn((n, d), generator=g, device=dev, dtype=torch.float32)
+    else:
+        gc = torch.Generator(device=dev)
+        gc.manual_seed(centers_seed)
+        cen = torch.randn((n_centers, d), generator=gc, device=dev, dtype=torch.float32)
+        cen /= torch.linalg.vector_norm(cen, dim=1, keepdim=True)
+        X = torch.empty((n, d), device=dev, dtype=torch.float32)
+        step = 1 << 18
+        for s in range(0, n, step):
+            e = min(n, s + step)
+            a = torch.randint(0, n_centers, (e - s,), generator=g, device=dev)
+            X[s:e] = cen[a] + spread * torch.randn((e - s, d), generator=g, device=dev, dtype=torch.float32)
     X /= torch.linalg.vector_norm(X, dim=1, keepdim=True)
     return X.contiguous()
 
@@ -117,7 +138,7 @@ def main():
     dev = _native.require_device()
     nbits = 8
     log(f"[rank {rank}] generating {a.n}x{a.d} on {torch.cuda.get_device_name(dev)}")
-    X = synth(a.n, a.d, seed=rank, dev=dev)
+    X = synth(a.n, a.d, seed=rank, dev=dev, kind=a.data)
 
     # codebooks: rank 0 trains, everyone receives (replicated, §8e)
     C = torch.empty((a.M, 256, a.d // a.M), dtype=torch.float32, device=dev)
@@ -132,7 +153,8 @@ def main():
     codes = torch.empty((a.n, _native.pq_code_size(a.M, nbits)), dtype=torch.uint8, device=dev)
 
     def step():
-        _native.pq_encode(X, C, prep, nbits, exact=a.exact, out=codes)
+        _native.pq_encode(X, C, prep, nbits, exact=a.exact, out=codes,
+                          flags_extra=_native.MIVQ_PQ_LEGACY_MFMA if a.legacy else 0)
 
     for _ in range(a.warmup):
         step()
@@ -165,7 +187,8 @@ def main():
 
     adc = None
     if not a.no_adc:
-        adc = sharded.bench_adc(X, C, codes, nbits, rank, world, dev, nq=a.nq, k=a.k, gt_queries=a.gt_queries)
+        Q = synth(a.nq, a.d, seed=1_000_003, dev=dev, kind=a.data)
+        adc = sharded.bench_adc(X, C, codes, nbits, rank, world, dev, Q, k=a.k, gt_queries=a.gt_queries)
         if rank == 0:
             log(f"[rank 0] adc: {adc}")
 
@@ -188,14 +211,15 @@ def main():
             "scaling": "weak",
             "vs_baseline": None,
             "dtype": "f32",
-            "data": "synthetic: torch.randn on device (seed = rank), rows L2-normalised; codebooks from "
-                    "GPU k-means on the first 65,536 rows (seed 1234, 25 iterations)",
+            "data": f"synthetic {a.data} (see synth(): generated on device, seed = rank, rows L2-normalised); "
+                    "codebooks from GPU k-means on the first 65,536 rows (seed 1234, 25 iterations)",
             "config": {"workload": workload, "rows_per_gpu": a.n, "dim": a.d, "M": a.M, "nbits": nbits,
-                       "path": "exact" if a.exact else "mfma-filter+exact-recheck",
+                       "path": "exact" if a.exact else ("legacy-mfma" if a.legacy else "cs-mfma-filter+exact-recheck"),
+                       "data": a.data,
                        "parallelism": f"row-sharded x{world}"},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic_from_profile(workload),
-                         "kernel": "pq_encode_mfma_kernel + pq_resolve_kernel (one mivq_pq_encode call)",
+                         "kernel": "pq_encode_cs_kernel + pq_transpose_codes_kernel (one mivq_pq_encode call)",
                          "bytes_per_vector": bytes_per_vec, "kernel_ms": kern_ms},
             "cpu_baseline": cpu,
             "parity_sample": parity,

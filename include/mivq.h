@@ -44,6 +44,7 @@ extern "C" {
 /* PQ encode flags */
 #define MIVQ_PQ_AUTO 0u        /* fp16-MFMA candidate filter + exact fp32 re-check when supported */
 #define MIVQ_PQ_FORCE_EXACT 1u /* exact fp32 VALU scan of every centroid (canonical order)     */
+#define MIVQ_PQ_LEGACY_MFMA 2u /* diagnostic: subspace-looping MFMA kernel + separate resolve */
 
 /* Metric enum values follow faiss / haag_vq.utils.faiss_utils.MetricType (faiss_utils.py:3-5). */
 #define MIVQ_METRIC_INNER_PRODUCT 0
@@ -129,6 +130,24 @@ int mivq_rabitq_encode(const float* x, int64_t n, int32_t d, const float* centro
                        int32_t metric, uint8_t* codes, void* stream);
 int mivq_rabitq_decode(const uint8_t* codes, int64_t n, int32_t d, const float* centroid,
                        float* out, void* stream);
+
+/* ------------------------------------------------------ Extended RaBitQ (B bits)
+ * The element-wise / per-row steps of ExtendedRaBitQuantizer.compress / decompress
+ * (extended_rabitq.py:125-199), fp64 like the reference; the two D x D rotations between
+ * them (o . P and o_hat . P^T) are plain fp64 GEMMs issued by the host.
+ *   normalize : o = (x - c) / max(||x - c||, 1e-12), nrm = ||x - c||   (x f32 or f64)
+ *   quantize  : s = s_raw * sqrt(D); idx = searchsorted(mid-levels, s); t = <s,s_hat>/<s_hat,s_hat>
+ *               code row = MSB-first B-bit indices (ceil(D*B/8) bytes) ++ f32 nrm ++ f32 t
+ *   dequantize: o_hat = (levels[idx] / sqrt(D)) * t
+ *   finish    : x_hat = f32(y * nrm + c)  with y = o_hat . P^T */
+int mivq_extrabitq_normalize(const void* x, int32_t x_is_f64, int64_t n, int32_t d,
+                             const double* centroid, double* o, double* nrm, void* stream);
+int mivq_extrabitq_quantize(const double* s_raw, int64_t n, int32_t d, const double* levels,
+                            int32_t nbits, const double* nrm, uint8_t* codes, void* stream);
+int mivq_extrabitq_dequantize(const uint8_t* codes, int64_t n, int32_t d, const double* levels,
+                              int32_t nbits, double* o_hat, void* stream);
+int mivq_extrabitq_finish(const double* y, int64_t n, int32_t d, const uint8_t* codes,
+                          int32_t nbits, const double* centroid, float* out, void* stream);
 
 /* ------------------------------------------------------ ADC search
  * Flat asymmetric-distance search over PQ codes; the GPU counterpart of

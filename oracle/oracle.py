@@ -317,6 +317,10 @@ def exact_l2_topk(Q: np.ndarray, X: np.ndarray, k: int) -> np.ndarray:
 
 
 def cpu_threads() -> int:
+    """Threads the OpenMP oracle actually runs with (OMP_NUM_THREADS, else the affinity mask)."""
+    env = os.environ.get("OMP_NUM_THREADS", "").split(",")[0].strip()
+    if env.isdigit() and int(env) > 0:
+        return int(env)
     try:
         return len(os.sched_getaffinity(0))
     except AttributeError:  # pragma: no cover

@@ -67,6 +67,51 @@ def test_pq_encode_bit_exact(dev, oracle, n, d, M, nbits):
     np.testing.assert_array_equal(got, ref)
     got_exact = _h(_native.pq_encode(_t(X, dev), Cd, prep, nbits, exact=True))
     np.testing.assert_array_equal(got_exact, ref)
+    got_legacy = _h(_native.pq_encode(_t(X, dev), Cd, prep, nbits, flags_extra=_native.MIVQ_PQ_LEGACY_MFMA))
+    np.testing.assert_array_equal(got_legacy, ref)
+
+
+@pytest.mark.parametrize("kind", ["gaussian", "clustered", "duplicates"])
+def test_pq_encode_bit_exact_trained_codebooks(dev, oracle, kind):
+    """Codebooks trained on the data (many near-ties), 20k rows, both MFMA kernels."""
+    from haag_vq import _native
+    from haag_vq.methods._kmeans import train_pq
+
+    rng = np.random.default_rng(11)
+    n, d, M = 20000, 1536, 16
+    if kind == "gaussian":
+        X = rng.standard_normal((n, d)).astype(np.float32)
+    else:
+        cen = rng.standard_normal((64, d)).astype(np.float32)
+        X = cen[rng.integers(0, 64, n)] + 0.02 * rng.standard_normal((n, d)).astype(np.float32)
+        if kind == "duplicates":
+            X[1::2] = X[0::2]  # every row twice
+    X /= np.linalg.norm(X, axis=1, keepdims=True)
+    Xd = _t(X, dev)
+    C = train_pq(Xd, M, 8, niter=10)
+    ref = oracle.pq_encode(X, _h(C))
+    prep = _native.pq_prepare(C, 8)
+    np.testing.assert_array_equal(_h(_native.pq_encode(Xd, C, prep, 8)), ref)
+    np.testing.assert_array_equal(_h(_native.pq_encode(Xd, C, prep, 8, flags_extra=_native.MIVQ_PQ_LEGACY_MFMA)), ref)
+
+
+@pytest.mark.parametrize("nbits", [1, 2, 4, 8])
+def test_extrabitq_kernels_match_reference_fixture(dev, golden_dir, nbits):
+    """Device encode/decode of the reference's ExtendedRaBitQuantizer model state."""
+    from haag_vq import _native
+
+    e = np.load(golden_dir / "extrabitq_golden.npz")
+    X = e["X"]
+    tag = f"b{nbits}"
+    c, P, lv = (_t(e[f"{tag}_{k}"], dev) for k in ("c", "P", "levels"))
+    codes = _h(_native.extrabitq_encode(_t(X, dev), c, P, lv, nbits))
+    ref = e[f"{tag}_codes"]
+    ib = (X.shape[1] * nbits + 7) // 8
+    # fp64 GEMM order differs from numpy: index bytes may differ only at level midpoints
+    assert (codes[:, :ib] != ref[:, :ib]).mean() < 1e-3
+    np.testing.assert_allclose(codes[:, ib:].copy().view(np.float32), ref[:, ib:].copy().view(np.float32), rtol=1e-6)
+    rec = _h(_native.extrabitq_decode(_t(ref, dev), c, P, lv, nbits))
+    np.testing.assert_allclose(rec, e[f"{tag}_recon"], rtol=1e-5, atol=1e-6)
 
 
 def test_pq_encode_extreme_rows_fall_back_exactly(dev, oracle):

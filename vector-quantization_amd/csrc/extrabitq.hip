@@ -55,29 +55,30 @@ __global__ __launch_bounds__(256) void erq_quantize_kernel(const double* __restr
     uint8_t* code = codes + row * cs;
     const double sq = sqrt((double)d);
     double num = 0.0, den = 0.0;
-    // zero the index bytes (bits are OR-ed in below)
-    for (int b = lane; b < ib; b += 64) code[b] = 0;
-    __syncthreads();
-    for (int j = lane; j < d; j += 64) {
-        const double s = __dmul_rn(s_raw[row * d + j], sq);
-        int idx = 0;
-        for (int q = 0; q + 1 < L; ++q) {
-            const double mid = __dmul_rn(0.5, __dadd_rn(levels[q], levels[q + 1]));
-            idx += (mid < s) ? 1 : 0;
-        }
-        const double sh = levels[idx];
-        num = __fma_rn(s, sh, num);
-        den = __fma_rn(sh, sh, den);
-        // MSB-first bit stream: bit (j*nbits + u) of the row holds bit (nbits-1-u) of idx
-        for (int u = 0; u < nbits; ++u) {
-            if ((idx >> (nbits - 1 - u)) & 1) {
-                const int gb = j * nbits + u;
-                atomicOr(reinterpret_cast<unsigned int*>(code + (gb >> 3 & ~3)) - 0 + 0,
-                         0u);  // placeholder keeps the address computation visible to the compiler
-                __hip_atomic_fetch_or(reinterpret_cast<unsigned int*>(reinterpret_cast<uintptr_t>(code + (gb >> 3)) & ~(uintptr_t)3),
-                                      (unsigned int)(0x80u >> (gb & 7)) << (8 * ((reinterpret_cast<uintptr_t>(code + (gb >> 3))) & 3)),
-                                      __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    // lane owns groups of 8 dims: 8 B-bit indices are exactly nbits whole bytes of the
+    // MSB-first stream (np.packbits order), bits past d*nbits stay 0
+    const int groups = (d + 7) / 8;
+    for (int g = lane; g < groups; g += 64) {
+        uint64_t bits = 0;
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+            const int j = g * 8 + u;
+            int idx = 0;
+            if (j < d) {
+                const double s = __dmul_rn(s_raw[row * d + j], sq);
+                for (int q = 0; q + 1 < L; ++q) {
+                    const double mid = __dmul_rn(0.5, __dadd_rn(levels[q], levels[q + 1]));
+                    idx += (mid < s) ? 1 : 0;  // searchsorted(side="left")
+                }
+                const double sh = levels[idx];
+                num = __fma_rn(s, sh, num);
+                den = __fma_rn(sh, sh, den);
             }
+            bits = (bits << nbits) | (uint64_t)idx;
+        }
+        for (int b = 0; b < nbits; ++b) {
+            const int byte = g * nbits + b;
+            if (byte < ib) code[byte] = (uint8_t)(bits >> (8 * (nbits - 1 - b)));
         }
     }
     num = wave_sum_d(num);

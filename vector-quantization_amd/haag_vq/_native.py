@@ -32,6 +32,7 @@ MIVQ_ERR_HIP = -3
 MIVQ_ERR_WORKSPACE = -4
 MIVQ_PQ_AUTO = 0
 MIVQ_PQ_FORCE_EXACT = 1
+MIVQ_PQ_LEGACY_MFMA = 2
 METRIC_INNER_PRODUCT = 0
 METRIC_L2 = 1
 NO_ID = 0xFFFFFFFF
@@ -58,6 +59,10 @@ SIGNATURES = {
     "mivq_sq_decode_f64": (_c.c_int, [_vp, _i64, _i32, _vp, _vp, _i32, _vp, _vp]),
     "mivq_rabitq_encode": (_c.c_int, [_vp, _i64, _i32, _vp, _i32, _vp, _vp]),
     "mivq_rabitq_decode": (_c.c_int, [_vp, _i64, _i32, _vp, _vp, _vp]),
+    "mivq_extrabitq_normalize": (_c.c_int, [_vp, _i32, _i64, _i32, _vp, _vp, _vp, _vp]),
+    "mivq_extrabitq_quantize": (_c.c_int, [_vp, _i64, _i32, _vp, _i32, _vp, _vp, _vp]),
+    "mivq_extrabitq_dequantize": (_c.c_int, [_vp, _i64, _i32, _vp, _i32, _vp, _vp]),
+    "mivq_extrabitq_finish": (_c.c_int, [_vp, _i64, _i32, _vp, _i32, _vp, _vp, _vp]),
     "mivq_adc_lut": (_c.c_int, [_vp, _i64, _i32, _i32, _i32, _vp, _i32, _vp, _vp]),
     "mivq_adc_search_workspace_bytes": (_sz, [_i64, _i64, _i32, _i32, _i32]),
     "mivq_adc_search": (_c.c_int, [_vp, _i64, _vp, _i64, _i32, _i32, _i32, _i64, _vp, _sz, _vp, _vp, _vp]),
@@ -179,7 +184,7 @@ def pq_prepare(centroids: torch.Tensor, nbits: int) -> torch.Tensor:
 
 
 def pq_encode(x: torch.Tensor, centroids: torch.Tensor, prep: torch.Tensor, nbits: int,
-              exact: bool = False, out: Optional[torch.Tensor] = None) -> torch.Tensor:
+              exact: bool = False, out: Optional[torch.Tensor] = None, flags_extra: int = 0) -> torch.Tensor:
     _check(x, "x", torch.float32, 2)
     _check(centroids, "centroids", torch.float32, 3)
     n, d = x.shape
@@ -195,7 +200,7 @@ def pq_encode(x: torch.Tensor, centroids: torch.Tensor, prep: torch.Tensor, nbit
             raise ValueError(f"out shape {tuple(out.shape)} != {(n, cs)}")
     nb = load_library().mivq_pq_encode_workspace_bytes(n, d, M, nbits)
     ws = workspace(nb, x.device)
-    flags = MIVQ_PQ_FORCE_EXACT if exact else MIVQ_PQ_AUTO
+    flags = (MIVQ_PQ_FORCE_EXACT if exact else MIVQ_PQ_AUTO) | flags_extra
     _call("mivq_pq_encode", _ptr(x), n, d, M, nbits, _ptr(centroids), _ptr(prep), _ptr(ws), ws.numel(),
           _ptr(out), flags, _stream())
     return out
@@ -305,6 +310,46 @@ def rabitq_decode(codes: torch.Tensor, d: int, centroid: Optional[torch.Tensor])
     n = codes.shape[0]
     out = torch.empty((n, d), dtype=torch.float32, device=codes.device)
     _call("mivq_rabitq_decode", _ptr(codes), n, d, _ptr(centroid), _ptr(out), _stream())
+    return out
+
+
+# ----------------------------------------------------------------- Extended RaBitQ
+def extrabitq_code_size(d: int, nbits: int) -> int:
+    return (d * nbits + 7) // 8 + 8
+
+
+def extrabitq_encode(x: torch.Tensor, c: torch.Tensor, P: torch.Tensor, levels: torch.Tensor,
+                     nbits: int) -> torch.Tensor:
+    """Codes of ExtendedRaBitQuantizer.compress; the o . P rotation is an fp64 library GEMM."""
+    if x.dtype not in (torch.float32, torch.float64):
+        raise ValueError(f"extrabitq: unsupported dtype {x.dtype}")
+    _check(x, "x", x.dtype, 2)
+    for t, nm in ((c, "c"), (levels, "levels")):
+        _check(t, nm, torch.float64, 1)
+    _check(P, "P", torch.float64, 2)
+    n, d = x.shape
+    o = torch.empty((n, d), dtype=torch.float64, device=x.device)
+    nrm = torch.empty((n,), dtype=torch.float64, device=x.device)
+    _call("mivq_extrabitq_normalize", _ptr(x), 1 if x.dtype == torch.float64 else 0, n, d, _ptr(c), _ptr(o),
+          _ptr(nrm), _stream())
+    s_raw = (o @ P).contiguous()
+    codes = torch.empty((n, extrabitq_code_size(d, nbits)), dtype=torch.uint8, device=x.device)
+    _call("mivq_extrabitq_quantize", _ptr(s_raw), n, d, _ptr(levels), nbits, _ptr(nrm), _ptr(codes), _stream())
+    return codes
+
+
+def extrabitq_decode(codes: torch.Tensor, c: torch.Tensor, P: torch.Tensor, levels: torch.Tensor,
+                     nbits: int) -> torch.Tensor:
+    _check(codes, "codes", torch.uint8, 2)
+    n = codes.shape[0]
+    d = P.shape[0]
+    if codes.shape[1] != extrabitq_code_size(d, nbits):
+        raise ValueError(f"codes have {codes.shape[1]} bytes per row, expected {extrabitq_code_size(d, nbits)}")
+    o_hat = torch.empty((n, d), dtype=torch.float64, device=codes.device)
+    _call("mivq_extrabitq_dequantize", _ptr(codes), n, d, _ptr(levels), nbits, _ptr(o_hat), _stream())
+    y = (o_hat @ P.T).contiguous()
+    out = torch.empty((n, d), dtype=torch.float32, device=codes.device)
+    _call("mivq_extrabitq_finish", _ptr(y), n, d, _ptr(codes), nbits, _ptr(c), _ptr(out), _stream())
     return out
 
 

@@ -75,13 +75,10 @@ def sharded_exact_search(Q: torch.Tensor, X: torch.Tensor, k: int, id_offset: in
 
 
 def bench_adc(X: torch.Tensor, C: torch.Tensor, codes: torch.Tensor, nbits: int, rank: int, world: int,
-              dev: torch.device, nq: int = 1000, k: int = 10, gt_queries: int = 100, reps: int = 3) -> dict:
+              dev: torch.device, Q: torch.Tensor, k: int = 10, gt_queries: int = 100, reps: int = 3) -> dict:
     """ADC queries/s and recall@k of the sharded index (bench.py's second leg)."""
     n, d = X.shape
-    g = torch.Generator(device=dev)
-    g.manual_seed(1_000_003)
-    Q = torch.randn((nq, d), generator=g, device=dev, dtype=torch.float32)
-    Q /= torch.linalg.vector_norm(Q, dim=1, keepdim=True)
+    nq = Q.shape[0]
     broadcast_(Q)
     off = rank * n
     u8 = codes if nbits == 8 else _native.pq_unpack(codes, C.shape[0], nbits)

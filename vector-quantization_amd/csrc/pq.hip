@@ -18,6 +18,7 @@
 //     (or fp16 overflow): flagged and settled by pq_resolve with the exact scan.  Codes
 //     are therefore identical to the canonical (oracle) codes, not "mostly".
 #include "mivq_common.h"
+#include "pq_internal.h"
 
 #include <math.h>
 
@@ -386,262 +387,6 @@ __global__ __launch_bounds__(512, 2) void pq_encode_mfma_kernel(
     for (int64_t e = tid; e < bytes; e += 512) dst[e] = cstage[e];
 }
 
-// --------------------------------------------------- codebook-stationary MFMA encode
-// Workgroup (chunk, m) owns subspace m for rows [chunk*R, (chunk+1)*R).  For its whole life
-// LDS holds (a) the fp16 operand image of C_m (8*KS KiB, fragment order), (b) the exact fp32
-// C_m with rows padded to dsub+4 floats (conflict-free 16-B row reads), (c) the scaled
-// accumulator init, (d) one 2*HALF-float row scratch per wave.  Each wave streams 32-row
-// blocks ("vb"): 16-B fragment loads of x straight to registers (one vb prefetched ahead),
-// 6*8 MFMAs per vb (KS=6), packed top-3 per lane, then
-//   1 candidate  -> done;
-//   2 candidates -> canonical chain of both, split across the lane pair (c from LDS);
-//   >= 3, or a row the filter cannot bound (fp16 overflow, NaN, tiny) -> canonical scan of
-//      all 256 centroids by the whole wave (c from LDS, x broadcast through the scratch).
-// Codes go to a transposed (M, n) scratch (32 contiguous bytes per vb) and
-// pq_transpose_codes_kernel writes the (n, M) layout.
-constexpr int kCsRows = 16384;  // rows per workgroup (R)
-
-__device__ __forceinline__ void lds_fence() {
-    // lgkmcnt(0): this wave's LDS writes have landed before other lanes read them
-    __builtin_amdgcn_s_waitcnt(0xC07F);
-    __builtin_amdgcn_wave_barrier();
-}
-
-template <int KS>
-__global__ __launch_bounds__(512, 2) void pq_encode_cs_kernel(
-    const float* __restrict__ x, int64_t n, int d, int M, int dsub, int64_t rows_per_wg,
-    const float* __restrict__ C, const float* __restrict__ cn, const half8* __restrict__ img,
-    const float* __restrict__ hinit, const float4* __restrict__ bnd, uint8_t* __restrict__ codesT) {
-    constexpr int FR = 8 * KS * 64;
-    constexpr int HALF = 8 * KS;
-    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-    const int LDR = dsub + 4;
-    half8* cimg = reinterpret_cast<half8*>(smem);                                  // FR * 16 B
-    float* c32 = reinterpret_cast<float*>(smem + FR * 16);                         // 256 * LDR
-    float* hb = c32 + 256 * LDR;                                                   // 256
-    float* xsc = hb + 256;                                                         // 8 * 2*HALF
-
-    const int tid = threadIdx.x;
-    const int w = tid >> 6, l = tid & 63;
-    const int r = l & 31, h = l >> 5;
-    const int m = (int)(blockIdx.x % M);
-    const int64_t chunk = blockIdx.x / M;
-    const int64_t r0 = chunk * rows_per_wg;
-    const int64_t r1 = min(n, r0 + rows_per_wg);
-
-    // ---- stage the subspace's codebook (once per workgroup)
-    {
-        const half8* src = img + (int64_t)m * FR;
-        for (int f = tid; f < FR; f += 512) cimg[f] = src[f];
-        const float* Cm = C + (int64_t)m * 256 * dsub;
-        const int q4 = dsub >> 2;  // float4 per row
-        for (int e = tid; e < 256 * q4; e += 512) {
-            const int k = e / q4, q = e % q4;
-            *reinterpret_cast<float4*>(c32 + k * LDR + 4 * q) =
-                *reinterpret_cast<const float4*>(Cm + (int64_t)k * dsub + 4 * q);
-        }
-        if (tid < 256) hb[tid] = hinit[(int64_t)m * 256 + tid];
-    }
-    __syncthreads();
-
-    const float4 bm = bnd[m];
-    const float sigma = bm.x;
-    const float* cnm = cn + (int64_t)m * 256;
-    const int h_begin = h * HALF;
-    const int nchunk = max(0, min(HALF, dsub - h_begin)) >> 2;
-    float* scratch = xsc + w * 2 * HALF;
-
-    float4 xc[HALF / 4];
-    float4 xn_[HALF / 4];
-    auto load_x = [&](int64_t vb, float4* dst) {
-        const int64_t row = vb * 32 + r;
-        const bool ok = row < r1;
-        const float* src = x + (ok ? row : 0) * (int64_t)d + (int64_t)m * dsub + h_begin;
-#pragma unroll
-        for (int i = 0; i < HALF / 4; ++i)
-            dst[i] = (ok && i < nchunk) ? *reinterpret_cast<const float4*>(src + 4 * i) : make_float4(0.f, 0.f, 0.f, 0.f);
-    };
-
-    const int64_t vb_first = r0 / 32 + w;
-    const int64_t vb_end = (r1 + 31) / 32;
-    if (vb_first < vb_end) load_x(vb_first, xc);
-    for (int64_t vb = vb_first; vb < vb_end; vb += kWaves) {
-        const int64_t nvb = vb + kWaves;
-        if (nvb < vb_end) load_x(nvb, xn_);
-        half8 bf[KS];
-        float xx = 0.0f;
-#pragma unroll
-        for (int ks = 0; ks < KS; ++ks) {
-            const float4 a = xc[2 * ks], b = xc[2 * ks + 1];
-            xx = __builtin_fmaf(a.x, a.x, xx); xx = __builtin_fmaf(a.y, a.y, xx);
-            xx = __builtin_fmaf(a.z, a.z, xx); xx = __builtin_fmaf(a.w, a.w, xx);
-            xx = __builtin_fmaf(b.x, b.x, xx); xx = __builtin_fmaf(b.y, b.y, xx);
-            xx = __builtin_fmaf(b.z, b.z, xx); xx = __builtin_fmaf(b.w, b.w, xx);
-            half8 v;
-            v[0] = (_Float16)(sigma * a.x); v[1] = (_Float16)(sigma * a.y);
-            v[2] = (_Float16)(sigma * a.z); v[3] = (_Float16)(sigma * a.w);
-            v[4] = (_Float16)(sigma * b.x); v[5] = (_Float16)(sigma * b.y);
-            v[6] = (_Float16)(sigma * b.z); v[7] = (_Float16)(sigma * b.w);
-            bf[ks] = v;
-        }
-        xx += __shfl_xor(xx, 32);
-        float t1 = -INFINITY, t2 = -INFINITY, t3 = -INFINITY;
-#pragma unroll
-        for (int cb = 0; cb < 8; ++cb) {
-            floatx16 acc;
-#pragma unroll
-            for (int q = 0; q < 4; ++q) {
-                const float4 hv = *reinterpret_cast<const float4*>(hb + cb * 32 + 8 * q + 4 * h);
-                acc[4 * q + 0] = hv.x; acc[4 * q + 1] = hv.y;
-                acc[4 * q + 2] = hv.z; acc[4 * q + 3] = hv.w;
-            }
-#pragma unroll
-            for (int ks = 0; ks < KS; ++ks)
-                acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(cimg[(cb * KS + ks) * 64 + l], bf[ks], acc, 0, 0, 0);
-#pragma unroll
-            for (int i = 0; i < 16; ++i)
-                top3_insert(t1, t2, t3, pack_idx(acc[i], (uint32_t)(cb * 32 + (i & 3) + 8 * (i >> 2))));
-        }
-        const uint32_t hbit = (uint32_t)h << 2;
-        t1 = __uint_as_float(__float_as_uint(t1) | hbit);
-        t2 = __uint_as_float(__float_as_uint(t2) | hbit);
-        t3 = __uint_as_float(__float_as_uint(t3) | hbit);
-        {
-            const float p1 = __shfl_xor(t1, 32), p2 = __shfl_xor(t2, 32), p3 = __shfl_xor(t3, 32);
-            top3_insert(t1, t2, t3, p1);
-            top3_insert(t1, t2, t3, p2);
-            top3_insert(t1, t2, t3, p3);
-        }
-        const float Xs = sigma * sqrtf(xx) * (1.0f + 1e-5f);
-        const float W = bm.y * Xs + bm.z;
-        const float thr = t1 - W;
-        // the filter bound needs finite f16 operands (|x~| <= Xs < 65504) and normal-range
-        // rows; anything else is settled by the canonical scan
-        const bool bad = !(Xs < 65000.0f) || !(Xs > 1e-12f) || !isfinite(t1) || !isfinite(W);
-        const int ncand = bad ? 3 : 1 + (t2 >= thr) + (t3 >= thr);
-        const int k1 = (int)(__float_as_uint(t1) & 0xFFu);
-        const int k2 = (int)(__float_as_uint(t2) & 0xFFu);
-        int code = k1;
-        if (__any(ncand == 2)) {
-            const bool need = (ncand == 2);
-            float carry = 0.0f, dot1 = 0.0f, dot2 = 0.0f;
-#pragma unroll
-            for (int phase = 0; phase < 3; ++phase) {
-                const bool active = need && ((h == 0 && phase < 2) || (h == 1 && phase > 0));
-                const int kk = (h == 0) ? (phase == 0 ? k1 : k2) : (phase == 1 ? k1 : k2);
-                float acc = (h == 0) ? 0.0f : carry;
-                if (active) {
-                    const float* crow = c32 + kk * LDR + h_begin;
-#pragma unroll
-                    for (int i = 0; i < HALF / 4; ++i) {
-                        if (i < nchunk) {
-                            const float4 cv = *reinterpret_cast<const float4*>(crow + 4 * i);
-                            const float4 xv = xc[i];
-                            acc = __builtin_fmaf(xv.x, cv.x, acc);
-                            acc = __builtin_fmaf(xv.y, cv.y, acc);
-                            acc = __builtin_fmaf(xv.z, cv.z, acc);
-                            acc = __builtin_fmaf(xv.w, cv.w, acc);
-                        }
-                    }
-                }
-                const float other = __shfl_xor(acc, 32);
-                if (h == 1) {
-                    carry = other;
-                    if (phase == 1) dot1 = acc;
-                    if (phase == 2) dot2 = acc;
-                }
-            }
-            if (need && h == 1) {
-                const float s1 = __builtin_fmaf(-2.0f, dot1, cnm[k1]);
-                const float s2 = __builtin_fmaf(-2.0f, dot2, cnm[k2]);
-                code = (s2 < s1 || (s2 == s1 && k2 < k1)) ? k2 : k1;
-            }
-            code = __shfl(code, (l & 31) + 32);
-        }
-        // canonical scan of all 256 centroids for the rows the filter could not settle
-        unsigned long long full = __ballot(ncand >= 3 && h == 0);
-        while (full) {
-            const int rr = __builtin_ctzll(full);
-            full &= full - 1;
-            if (r == rr) {  // lanes rr and rr+32 publish their halves of the row
-#pragma unroll
-                for (int i = 0; i < HALF / 4; ++i)
-                    *reinterpret_cast<float4*>(scratch + h_begin + 4 * i) = xc[i];
-            }
-            lds_fence();
-            float acc4[4] = {0.f, 0.f, 0.f, 0.f};
-            for (int t = 0; t < dsub; t += 4) {
-                const float4 xv = *reinterpret_cast<const float4*>(scratch + t);
-#pragma unroll
-                for (int j = 0; j < 4; ++j) {
-                    const float4 cv = *reinterpret_cast<const float4*>(c32 + (l + 64 * j) * LDR + t);
-                    acc4[j] = __builtin_fmaf(xv.x, cv.x, acc4[j]);
-                    acc4[j] = __builtin_fmaf(xv.y, cv.y, acc4[j]);
-                    acc4[j] = __builtin_fmaf(xv.z, cv.z, acc4[j]);
-                    acc4[j] = __builtin_fmaf(xv.w, cv.w, acc4[j]);
-                }
-            }
-            float bs = INFINITY;
-            int bk = l;
-#pragma unroll
-            for (int j = 0; j < 4; ++j) {
-                const float s = __builtin_fmaf(-2.0f, acc4[j], cnm[l + 64 * j]);
-                if (s < bs) { bs = s; bk = l + 64 * j; }
-            }
-#pragma unroll
-            for (int o = 32; o > 0; o >>= 1) {
-                const float os = __shfl_xor(bs, o);
-                const int ok = __shfl_xor(bk, o);
-                if (os < bs || (os == bs && ok < bk)) { bs = os; bk = ok; }
-            }
-            if (r == rr) code = (bs < INFINITY) ? bk : 0;
-            lds_fence();  // scratch is rewritten by the next flagged row
-        }
-        if (h == 0) {
-            const int64_t row = vb * 32 + r;
-            if (row < r1) codesT[(int64_t)m * n + row] = (uint8_t)code;
-        }
-        if (nvb < vb_end) {
-#pragma unroll
-            for (int i = 0; i < HALF / 4; ++i) xc[i] = xn_[i];
-        }
-    }
-}
-
-// (M, n) -> (n, M): one block per 256 rows, the tile goes through LDS.
-__global__ __launch_bounds__(256) void pq_transpose_codes_kernel(const uint8_t* __restrict__ codesT, int64_t n, int M,
-                                                                 uint8_t* __restrict__ codes) {
-    extern __shared__ __attribute__((aligned(16))) uint8_t tile[];  // [256][M]
-    const int64_t r0 = (int64_t)blockIdx.x * 256;
-    const int rows = (int)min<int64_t>(256, n - r0);
-    for (int e = threadIdx.x; e < M * 256; e += 256) {
-        const int mm = e / 256, rr = e % 256;
-        if (rr < rows) tile[rr * M + mm] = codesT[(int64_t)mm * n + r0 + rr];
-    }
-    __syncthreads();
-    for (int e = threadIdx.x; e < rows * M; e += 256) codes[r0 * M + e] = tile[e];
-}
-
-int cs_smem_bytes(int KS, int dsub) {
-    return 8 * KS * 64 * 16 + 256 * (dsub + 4) * 4 + 256 * 4 + kWaves * 2 * 8 * KS * 4;
-}
-
-template <int KS>
-hipError_t launch_cs(const float* x, int64_t n, int d, int M, int dsub, const float* C, const float* cn,
-                     const half8* img, const float* hinit, const float4* bnd, uint8_t* codesT, hipStream_t st) {
-    const int smem = cs_smem_bytes(KS, dsub);
-    auto kern = pq_encode_cs_kernel<KS>;
-    hipError_t e = hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, smem);
-    if (e != hipSuccess) return e;
-    // enough workgroups to cover the chip even for small n; R a multiple of 32
-    int64_t R = kCsRows;
-    while (R > 256 && ceil_div(n, R) * M < 1024) R /= 2;
-    const int64_t grid = ceil_div(n, R) * M;
-    hipLaunchKernelGGL(kern, dim3((unsigned)grid), dim3(512), smem, st, x, n, d, M, dsub, R, C, cn, img, hinit, bnd,
-                       codesT);
-    return hipGetLastError();
-}
-
 // Settles the (row, subspace) pairs the filter flagged: one block (256 threads = one lane per
 // centroid) runs the canonical chain for every centroid and takes the first minimum.
 __global__ __launch_bounds__(256) void pq_resolve_kernel(
@@ -878,23 +623,9 @@ extern "C" int mivq_pq_encode(const float* x, int64_t n, int32_t d, int32_t M, i
                        !(flags_in & MIVQ_PQ_LEGACY_MFMA);
     const bool mfma_ok = L.mfma && aligned && L.ks <= 8 && !exact_only && mfma_smem_bytes(L.ks, M) <= 160 * 1024;
     if (cs_ok) {
-        const half8* img = reinterpret_cast<const half8*>(p + L.img);
-        const float* hinit = reinterpret_cast<const float*>(p + L.hinit);
-        const float4* bnd = reinterpret_cast<const float4*>(p + L.bnd);
-        hipError_t e = hipSuccess;
-        switch (L.ks) {
-            case 1: e = launch_cs<1>(x, n, d, M, L.dsub, centroids, cn, img, hinit, bnd, codesT, st); break;
-            case 2: e = launch_cs<2>(x, n, d, M, L.dsub, centroids, cn, img, hinit, bnd, codesT, st); break;
-            case 3: e = launch_cs<3>(x, n, d, M, L.dsub, centroids, cn, img, hinit, bnd, codesT, st); break;
-            case 4: e = launch_cs<4>(x, n, d, M, L.dsub, centroids, cn, img, hinit, bnd, codesT, st); break;
-            case 5: e = launch_cs<5>(x, n, d, M, L.dsub, centroids, cn, img, hinit, bnd, codesT, st); break;
-            case 6: e = launch_cs<6>(x, n, d, M, L.dsub, centroids, cn, img, hinit, bnd, codesT, st); break;
-        }
+        const hipError_t e = launch_pq_encode_cs(L.ks, x, n, d, M, L.dsub, centroids, cn, p + L.img,
+                                                 reinterpret_cast<const float*>(p + L.hinit), p + L.bnd, codesT, u8, st);
         if (e != hipSuccess) return set_error(MIVQ_ERR_HIP, "pq_encode_cs: %s", hipGetErrorString(e));
-        hipLaunchKernelGGL(pq_transpose_codes_kernel, dim3((unsigned)ceil_div(n, 256)), dim3(256), (size_t)256 * M, st,
-                           codesT, n, M, u8);
-        int rc = check_launch("pq_transpose_codes");
-        if (rc) return rc;
     } else if (mfma_ok) {
         const half8* img = reinterpret_cast<const half8*>(p + L.img);
         const float* hinit = reinterpret_cast<const float*>(p + L.hinit);

@@ -1,0 +1,17 @@
+// pq_internal.h — kernels of pq_encode_cs.hip dispatched from pq.hip.
+#pragma once
+
+#include "mivq_common.h"
+
+namespace mivq {
+
+// Dynamic LDS bytes of the codebook-stationary encode for KS k-steps and dsub.
+int cs_smem_bytes(int KS, int dsub);
+
+// Codebook-stationary fp16-MFMA encode with exact re-check (KS in 1..6).  Writes the
+// transposed codes into codesT (M, n) and then the (n, M) byte codes into `codes`.
+hipError_t launch_pq_encode_cs(int KS, const float* x, int64_t n, int d, int M, int dsub, const float* C,
+                               const float* cn, const void* img, const float* hinit, const void* bnd,
+                               uint8_t* codesT, uint8_t* codes, hipStream_t st);
+
+}  // namespace mivq

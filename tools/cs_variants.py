@@ -1,0 +1,93 @@
+"""Time the codebook-stationary encode kernel with parts of its work removed.
+
+usage: python tools/cs_variants.py [--n 1000000] [--reps 10]
+Builds tools/build/libcsvar.so (hipcc, gfx950) unless it exists, then prints one line per
+variant: device ms per launch (HIP events on the launch stream).
+"""
+import argparse
+import ctypes
+import subprocess
+import sys
+from pathlib import Path
+
+import torch
+
+ROOT = Path(__file__).resolve().parent.parent
+sys.path.insert(0, str(ROOT / "vector-quantization_amd"))
+sys.path.insert(0, str(ROOT))
+from haag_vq import _native  # noqa: E402
+from haag_vq.methods._kmeans import train_pq  # noqa: E402
+from bench import synth  # noqa: E402
+
+VARIANTS = {0: "full kernel", 1: "no 2-cand check", 2: "no full scan", 3: "no exact checks",
+            7: "no checks, max-only filter", 39: "no checks, max-only, 1 of 8 cb",
+            35: "no checks, top-3, 1 of 8 cb", 19: "loads + convert + store only"}
+
+
+def prep_layout(M, dsub, ksub=256):
+    """Byte offsets inside the mivq_pq_prepare buffer (mirror of PqPrepLayout, mivq_common.h)."""
+    al = lambda v: (v + 255) // 256 * 256  # noqa: E731
+    ks = (dsub + 15) // 16
+    L, off = {}, 0
+    L["cn"] = off; off = al(off + 4 * M * ksub)
+    L["ct"] = off; off = al(off + 4 * M * dsub * ksub)
+    L["img"] = off; off = al(off + M * 8 * ks * 64 * 8 * 2)
+    L["hinit"] = off; off = al(off + 4 * M * ksub)
+    L["bnd"] = off
+    return L
+
+
+def build():
+    so = ROOT / "tools" / "build" / "libcsvar.so"
+    src = ROOT / "tools" / "cs_variants.hip"
+    if not so.exists() or so.stat().st_mtime < max(src.stat().st_mtime, (ROOT / "vector-quantization_amd/csrc/pq_encode_cs.hip").stat().st_mtime):
+        so.parent.mkdir(exist_ok=True)
+        subprocess.check_call(["hipcc", "-O3", "-std=c++17", "--offload-arch=gfx950", "-fPIC", "-shared",
+                               "-ffp-contract=off", "-fvisibility=hidden", "-o", str(so), str(src)])
+    return ctypes.CDLL(str(so))
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--n", type=int, default=1_000_000)
+    ap.add_argument("--d", type=int, default=1536)
+    ap.add_argument("--M", type=int, default=16)
+    ap.add_argument("--reps", type=int, default=10)
+    ap.add_argument("--data", default="clustered")
+    a = ap.parse_args()
+    lib = build()
+    dev = _native.require_device()
+    X = synth(a.n, a.d, 0, dev, kind=a.data)
+    C = train_pq(X[:65536], a.M, 8, niter=25, seed=1234).contiguous()
+    prep = _native.pq_prepare(C, 8)
+    ref = _native.pq_encode(X, C, prep, 8)
+    dsub = a.d // a.M
+    L = prep_layout(a.M, dsub)
+    base = prep.data_ptr()
+    codesT = torch.empty((a.M, a.n), dtype=torch.uint8, device=dev)
+    st = torch.cuda.current_stream().cuda_stream
+    P = ctypes.c_void_p
+
+    def run(v):
+        rc = lib.cs_variant(ctypes.c_int(v), P(X.data_ptr()), ctypes.c_int64(a.n), ctypes.c_int(a.d), ctypes.c_int(a.M),
+                            ctypes.c_int(dsub), P(C.data_ptr()), P(base + L["cn"]), P(base + L["img"]),
+                            P(base + L["hinit"]), P(base + L["bnd"]), P(codesT.data_ptr()), P(st))
+        assert rc == 0, rc
+
+    for v, name in VARIANTS.items():
+        run(v)
+        torch.cuda.synchronize()
+        if v == 0:
+            ok = bool((codesT.t() == ref).all())
+        ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(a.reps)]
+        for s, e in ev:
+            s.record(); run(v); e.record()
+        torch.cuda.synchronize()
+        ms = sorted(s.elapsed_time(e) for s, e in ev)[a.reps // 2]
+        gbs = a.n * (4 * a.d + a.M) / (ms * 1e-3) / 1e9
+        print(f"V={v:2d} {name:32s} {ms:7.3f} ms  {gbs:7.0f} GB/s" + (f"  codes match library: {ok}" if v == 0 else ""),
+              flush=True)
+
+
+if __name__ == "__main__":
+    main()

@@ -1,6 +1,7 @@
 """Summarise rocprofv3 --pmc passes for one kernel: per-dispatch averages of each counter.
 
-usage: python tools/pmc_summary.py gpurun_out/pmc_<tag> <kernel-substring> [grid_size]
+usage: python tools/pmc_summary.py gpurun_out/pmc_<tag> <kernel-substring> [last_n]
+(last_n: only the last N matching dispatches of each pass, e.g. the timed bench steps)
 Prints counters and the derived HBM traffic (gfx950: FETCH_SIZE reads half the bytes of a
 wide coalesced stream -> x2, MI355X_MICROARCH.md §HBM; FETCH/WRITE_SIZE are in KiB).
 """
@@ -11,15 +12,15 @@ import sys
 from collections import defaultdict
 
 root, sub = sys.argv[1], sys.argv[2]
-grid = int(sys.argv[3]) if len(sys.argv) > 3 else None
+last_n = int(sys.argv[3]) if len(sys.argv) > 3 else None
 vals = defaultdict(list)
 durs = []
 for f in sorted(glob.glob(f"{root}/p*/run_counter_collection.csv")):
-    for r in csv.DictReader(open(f)):
-        if sub not in r["Kernel_Name"]:
-            continue
-        if grid is not None and int(r["Grid_Size"]) != grid:
-            continue
+    rows = [r for r in csv.DictReader(open(f)) if sub in r["Kernel_Name"]]
+    if last_n is not None:
+        ids = sorted({int(r["Dispatch_Id"]) for r in rows})[-last_n:]
+        rows = [r for r in rows if int(r["Dispatch_Id"]) in ids]
+    for r in rows:
         vals[r["Counter_Name"]].append(float(r["Counter_Value"]))
         durs.append((int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3)
 out = {k: sum(v) / len(v) for k, v in vals.items()}

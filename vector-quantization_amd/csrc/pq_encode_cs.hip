@@ -42,10 +42,16 @@ typedef float floatx16 __attribute__((ext_vector_type(16)));
 constexpr int kWaves = 8;  // 512 threads, 2 waves per SIMD
 constexpr int kThreads = kWaves * 64;
 
+// Keeps the three largest of a stream of packed scores.  Inline asm because the compiler
+// quiets every packed value (v_max_f32 v, v, v) before fmaxf / fmed3 in IEEE mode: the
+// values come out of integer bit operations.  They are never NaN here (a row whose scores
+// could be is routed to the exact scan by the `bad` test), so the quieting is pure cost.
+// The operands are plain VALU results, so no MFMA hazard is hidden from the compiler.
 __device__ __forceinline__ void top3_insert(float& t1, float& t2, float& t3, float v) {
-    const float n1 = fmaxf(t1, v);
-    const float n2 = __builtin_amdgcn_fmed3f(t1, t2, v);
-    const float n3 = __builtin_amdgcn_fmed3f(t2, t3, v);
+    float n1, n2, n3;
+    asm("v_max_f32 %0, %1, %2" : "=v"(n1) : "v"(t1), "v"(v));
+    asm("v_med3_f32 %0, %1, %2, %3" : "=v"(n2) : "v"(t1), "v"(t2), "v"(v));
+    asm("v_med3_f32 %0, %1, %2, %3" : "=v"(n3) : "v"(t2), "v"(t3), "v"(v));
     t1 = n1; t2 = n2; t3 = n3;
 }
 
@@ -73,7 +79,10 @@ __device__ __forceinline__ uint32_t cvt2(float a, float b) {
     return __builtin_bit_cast(uint32_t, h);
 }
 
-template <int KS>
+// V: profiling variants (tools/cs_variants.hip), 0 in the library.  Bits drop work and
+// produce wrong codes: 1 the 2-candidate checks, 2 the full scans, 4 the top-3 (max only),
+// 8 the MFMAs, 16 the whole filter, 32 all but the first 32 centroids.
+template <int KS, int V = 0>
 struct CsCtx {
     static constexpr int HALF = 8 * KS;
     static constexpr int NC = HALF / 4;  // float4 per lane-half
@@ -118,7 +127,7 @@ struct CsCtx {
 
         float t1 = -INFINITY, t2 = -INFINITY, t3 = -INFINITY;
 #pragma unroll
-        for (int cb = 0; cb < 8; ++cb) {
+        for (int cb = 0; cb < ((V & 16) ? 0 : (V & 32) ? 1 : 8); ++cb) {
             half8 a[KS];
 #pragma unroll
             for (int ks = 0; ks < KS; ++ks) a[ks] = cimg[(cb * KS + ks) * 64 + l];
@@ -130,10 +139,11 @@ struct CsCtx {
                 acc[4 * q + 2] = hv.z; acc[4 * q + 3] = hv.w;
             }
 #pragma unroll
-            for (int ks = 0; ks < KS; ++ks) acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(a[ks], bf[ks], acc, 0, 0, 0);
+            for (int ks = 0; ks < ((V & 8) ? 0 : KS); ++ks) acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(a[ks], bf[ks], acc, 0, 0, 0);
 #pragma unroll
             for (int i = 0; i < 16; ++i)
-                top3_insert(t1, t2, t3, pack_idx(acc[i], vmask, (uint32_t)(cb * 32 + (i & 3) + 8 * (i >> 2))));
+                if constexpr ((V & 4) != 0) asm("v_max_f32 %0, %0, %1" : "+v"(t1) : "v"(pack_idx(acc[i], vmask, (uint32_t)(cb * 32 + (i & 3) + 8 * (i >> 2)))));
+                else top3_insert(t1, t2, t3, pack_idx(acc[i], vmask, (uint32_t)(cb * 32 + (i & 3) + 8 * (i >> 2))));
         }
         const uint32_t hbit = (uint32_t)h << 2;
         t1 = __uint_as_float(__float_as_uint(t1) | hbit);
@@ -153,7 +163,16 @@ struct CsCtx {
         const int k1 = (int)(__float_as_uint(t1) & 0xFFu);
         const int k2 = (int)(__float_as_uint(t2) & 0xFFu);
         int code = k1;
-        if (__any(ncand == 2)) {
+        if constexpr ((V & 16) != 0) {  // keep the loads and conversions alive
+            uint32_t z = 0;
+#pragma unroll
+            for (int ks = 0; ks < KS; ++ks) {
+                const uint4 u = __builtin_bit_cast(uint4, bf[ks]);
+                z ^= u.x ^ u.y ^ u.z ^ u.w;
+            }
+            code ^= (int)(z & 0xFF);
+        }
+        if (!(V & 1) && __any(ncand == 2)) {
             const bool need = (ncand == 2);
             float carry = 0.0f, dot1 = 0.0f, dot2 = 0.0f;
 #pragma unroll
@@ -189,7 +208,7 @@ struct CsCtx {
             }
             code = __shfl(code, (l & 31) + 32);
         }
-        unsigned long long full = __ballot(ncand >= 3 && h == 0);
+        unsigned long long full = (V & 2) ? 0ull : __ballot(ncand >= 3 && h == 0);
         while (full) {
             const int rr = __builtin_ctzll(full);
             full &= full - 1;
@@ -233,7 +252,7 @@ struct CsCtx {
     }
 };
 
-template <int KS>
+template <int KS, int V = 0>
 __global__ __launch_bounds__(kThreads, 2) void pq_encode_cs_kernel(
     const float* __restrict__ x, int64_t n, int d, int M, int dsub, int64_t rows_per_wg,
     const float* __restrict__ C, const float* __restrict__ cn, const half8* __restrict__ img,
@@ -273,7 +292,7 @@ __global__ __launch_bounds__(kThreads, 2) void pq_encode_cs_kernel(
     }
     __syncthreads();
 
-    CsCtx<KS> c;
+    CsCtx<KS, V> c;
     c.l = tid & 63;
     c.r = c.l & 31;
     c.h = c.l >> 5;
@@ -344,11 +363,11 @@ int64_t pick_chunks(int64_t n, int M, int cus) {
     return best;
 }
 
-template <int KS>
+template <int KS, int V = 0>
 hipError_t launch_ks(const float* x, int64_t n, int d, int M, int dsub, const float* C, const float* cn,
                      const void* img, const float* hinit, const void* bnd, uint8_t* codesT, hipStream_t st) {
     const int smem = cs_smem_bytes(KS, dsub);
-    auto kern = pq_encode_cs_kernel<KS>;
+    auto kern = pq_encode_cs_kernel<KS, V>;
     hipError_t e = hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, smem);
     if (e != hipSuccess) return e;
     static thread_local int cus = 0;

@@ -5,14 +5,14 @@
 
 #define VARIANT(v)                                                                                     \
     case v:                                                                                           \
-        return (int)mivq::launch_ks<6, v>(x, n, d, M, dsub, C, cn, img, hinit, bnd, codesT, (hipStream_t)st);
+        return (int)mivq::launch_pq_encode_cs_v<6, v>(x, n, d, M, dsub, C, cn, img, hinit, bnd, codesT, items, counts, (hipStream_t)st);
 
 extern "C" __attribute__((visibility("default"))) int cs_variant(int V, const float* x, int64_t n, int d, int M,
                                                                   int dsub, const float* C, const float* cn,
                                                                   const void* img, const float* hinit,
-                                                                  const void* bnd, uint8_t* codesT, void* st) {
+                                                                  const void* bnd, uint8_t* codesT, void* items, void* counts, void* st) {
     switch (V) {
-        VARIANT(0) VARIANT(1) VARIANT(2) VARIANT(3) VARIANT(7) VARIANT(39) VARIANT(35) VARIANT(19)
+        VARIANT(0) VARIANT(1) VARIANT(2) VARIANT(4) VARIANT(8) VARIANT(17) VARIANT(33)
         default: return -1;
     }
 }

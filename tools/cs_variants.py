@@ -19,9 +19,9 @@ from haag_vq import _native  # noqa: E402
 from haag_vq.methods._kmeans import train_pq  # noqa: E402
 from bench import synth  # noqa: E402
 
-VARIANTS = {0: "full kernel", 1: "no 2-cand check", 2: "no full scan", 3: "no exact checks",
-            7: "no checks, max-only filter", 39: "no checks, max-only, 1 of 8 cb",
-            35: "no checks, top-3, 1 of 8 cb", 19: "loads + convert + store only"}
+VARIANTS = {0: "encode + resolve", 1: "encode only", 2: "resolve: pairs only", 4: "resolve: full scans only",
+            8: "resolve: gathers, no compute", 33: "encode only, 1 of 8 cb",
+            17: "loads + convert + tile + fragments only"}
 
 
 def prep_layout(M, dsub, ksub=256):
@@ -65,13 +65,16 @@ def main():
     L = prep_layout(a.M, dsub)
     base = prep.data_ptr()
     codesT = torch.empty((a.M, a.n), dtype=torch.uint8, device=dev)
+    items = torch.empty((a.M * a.n * 8,), dtype=torch.uint8, device=dev)
+    counts = torch.empty((a.M * a.n // 32 + 64, 2), dtype=torch.int32, device=dev)
     st = torch.cuda.current_stream().cuda_stream
     P = ctypes.c_void_p
 
     def run(v):
         rc = lib.cs_variant(ctypes.c_int(v), P(X.data_ptr()), ctypes.c_int64(a.n), ctypes.c_int(a.d), ctypes.c_int(a.M),
                             ctypes.c_int(dsub), P(C.data_ptr()), P(base + L["cn"]), P(base + L["img"]),
-                            P(base + L["hinit"]), P(base + L["bnd"]), P(codesT.data_ptr()), P(st))
+                            P(base + L["hinit"]), P(base + L["bnd"]), P(codesT.data_ptr()),
+                            P(items.data_ptr()), P(counts.data_ptr()), P(st))
         assert rc == 0, rc
 
     for v, name in VARIANTS.items():
@@ -79,6 +82,15 @@ def main():
         torch.cuda.synchronize()
         if v == 0:
             ok = bool((codesT.t() == ref).all())
+            counts.zero_()
+            run(v)
+            torch.cuda.synchronize()
+            c = counts.sum(0).tolist()
+            nz = counts[(counts.sum(1) > 0)].float()
+            print(f"per-workgroup items: {nz.shape[0]} groups, pairs mean {nz[:, 0].mean():.0f} max {nz[:, 0].max():.0f}, "
+                  f"full mean {nz[:, 1].mean():.0f} max {nz[:, 1].max():.0f}", flush=True)
+            print(f"resolve items: pairs {c[0]} ({c[0] / (a.n * a.M):.2%} of row-subspaces), "
+                  f"full {c[1]} ({c[1] / (a.n * a.M):.2%})", flush=True)
         ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(a.reps)]
         for s, e in ev:
             s.record(); run(v); e.record()

@@ -586,8 +586,10 @@ extern "C" size_t mivq_pq_encode_workspace_bytes(int64_t n, int32_t d, int32_t M
     if (n < 0 || M <= 0) return 0;
     size_t b = 0;
     if (nbits != 8) b += align_up((size_t)n * M, 256);                 // unpacked codes
-    b += align_up((size_t)ceil_div(n, 32) * M * sizeof(uint32_t), 256);  // filter flags
-    b += align_up((size_t)n * M, 256);                                 // transposed codes (cs path)
+    b += align_up((size_t)n * M, 256);  // transposed codes (cs path)
+    // cs path: n*M uint2 resolve items; legacy MFMA path: its filter flags (never both)
+    b += align_up(std::max((size_t)n * M * 8, (size_t)ceil_div(n, 32) * M * sizeof(uint32_t)), 256);
+    b += align_up(cs_counts_bytes(n, M), 256);  // cs path: list counts per workgroup
     return b;
 }
 
@@ -613,9 +615,12 @@ extern "C" int mivq_pq_encode(const float* x, int64_t n, int32_t d, int32_t M, i
     uint8_t* u8 = codes;
     size_t off = 0;
     if (nbits != 8) { u8 = ws; off = align_up((size_t)n * M, 256); }
-    uint32_t* fl = reinterpret_cast<uint32_t*>(ws + off);
-    off += align_up((size_t)ceil_div(n, 32) * M * sizeof(uint32_t), 256);
     uint8_t* codesT = ws + off;
+    off += align_up((size_t)n * M, 256);
+    uint32_t* fl = reinterpret_cast<uint32_t*>(ws + off);  // legacy path
+    void* items = ws + off;                                // cs path
+    off += align_up(std::max((size_t)n * M * 8, (size_t)ceil_div(n, 32) * M * sizeof(uint32_t)), 256);
+    void* counts = ws + off;
 
     const bool aligned = (reinterpret_cast<uintptr_t>(x) % 16 == 0) && (d % 4 == 0) && (L.dsub % 4 == 0);
     const bool exact_only = (flags_in & MIVQ_PQ_FORCE_EXACT) != 0;
@@ -624,7 +629,8 @@ extern "C" int mivq_pq_encode(const float* x, int64_t n, int32_t d, int32_t M, i
     const bool mfma_ok = L.mfma && aligned && L.ks <= 8 && !exact_only && mfma_smem_bytes(L.ks, M) <= 160 * 1024;
     if (cs_ok) {
         const hipError_t e = launch_pq_encode_cs(L.ks, x, n, d, M, L.dsub, centroids, cn, p + L.img,
-                                                 reinterpret_cast<const float*>(p + L.hinit), p + L.bnd, codesT, u8, st);
+                                                 reinterpret_cast<const float*>(p + L.hinit), p + L.bnd, codesT, items,
+                                                 counts, u8, st);
         if (e != hipSuccess) return set_error(MIVQ_ERR_HIP, "pq_encode_cs: %s", hipGetErrorString(e));
     } else if (mfma_ok) {
         const half8* img = reinterpret_cast<const half8*>(p + L.img);

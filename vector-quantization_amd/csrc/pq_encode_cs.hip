@@ -5,28 +5,34 @@
 // canonical encode of include/mivq.h bit for bit; the filter window W is derived in pq.hip
 // (pq_prep_mfma_kernel / the comment above pq_encode_mfma_kernel).
 //
-// Work decomposition.  Workgroup (chunk, m) owns subspace m for rows [chunk*R, (chunk+1)*R)
+// Work decomposition.  Workgroup (chunk, m) owns subspace m for rows [r0, r1) of one chunk
 // (blockIdx = chunk*M + m).  The number of chunks is chosen so that the grid is a whole
-// number of waves of workgroups over the CUs (one workgroup per CU: the LDS below).  For the
-// workgroup's whole life LDS holds
-//   cimg : the fp16 operand image of C_m, fragment order (8*KS KiB; ds_read_b128, no conflicts)
-//   c32  : the exact fp32 C_m, rows padded to dsub+4 floats (conflict-free 16-B row reads)
-//   hb   : the scaled accumulator init -|c|^2 * sigma * tau / 2
-//   cnl  : the canonical norms |c|^2 of C_m
-//   xsc  : one 2*HALF-float row scratch per wave (full canonical scans)
-// 8 waves (2 per SIMD) each stream 32-row blocks ("vb"): 16-B loads of x straight to
-// registers with the next vb prefetched (ping-pong register sets, no copies), 8*KS
-// v_mfma_f32_32x32x16_f16 per vb, a packed top-3 per lane (one v_and_or_b32 + max + 2 med3
-// per score), then
-//   1 candidate in the window  -> done;
-//   2 candidates               -> canonical fmaf chains of both, split across the lane pair,
-//                                 centroids from c32, x from the registers;
-//   >= 3, or a row the window cannot bound (fp16 overflow, NaN, tiny) -> canonical scan of all
-//                                 256 centroids by the whole wave from c32.
-// The only global loads inside the loop are the x prefetches: vmcnt retires in order, so any
-// later global load (a norm, a re-read of x) would make the wave wait for the prefetch too.
+// number of rounds of workgroups over the CUs (one workgroup per CU: the LDS below).
+//
+// Phase 1 (streaming).  LDS holds, for the workgroup's life,
+//   cimg : the fp16 operand image of C_m in fragment order (8*KS KiB; ds_read_b128)
+//   stg  : one fp16 x tile per wave, 32 rows x 16*KS halves, row pitch 32*KS+16 bytes
+//   hb   : the scaled accumulator init -|c|^2 * sigma * tau / 2;  cnl : |c|^2
+// 12 waves (3 per SIMD) each stream 32-row blocks ("vb").  x is read with buffer loads
+// whose wave-instruction covers whole row segments (floor(64/(dsub/4)) rows, e.g. 2 rows =
+// 768 bytes for dsub = 96; a lane-per-row fragment load touches 64 cache lines per
+// instruction and streams at less than half the rate), scaled by sigma, converted to fp16
+// and written to the wave's tile (tile rows past the range keep stale values: an MFMA
+// column depends on its own row only); the MFMA B fragments are read back from it.  The next
+// vb's loads are in flight while the current one is filtered: 8*KS v_mfma_f32_32x32x16_f16,
+// a packed top-3 per lane (one v_and_or_b32 + max + 2 med3 per score), the partner-lane
+// merge, then
+//   1 candidate in the window -> the code is written;
+//   2 candidates              -> (row, k1, k2) goes to the workgroup's pair list;
+//   >= 3 candidates, or a row the window cannot bound (fp16 overflow, NaN) -> full list.
+// Phase 2 (resolve).  The LDS is re-staged with the exact fp32 codebook, centroid pairs
+// (k, k+128) interleaved, and the workgroup settles its lists, one item per lane, with the
+// canonical fmaf chains: pairs compare their two candidates, full items scan all 256
+// centroids with v_pk_fma_f32 (two chains per instruction, LDS broadcast reads).  The x
+// sub-row is re-read from memory (about 11% of the rows on embedding-like data).
 // Codes go to a transposed (M, n) scratch (32 contiguous bytes per vb); a transpose kernel
-// writes the (n, M) layout.
+// writes the (n, M) layout.  Lists live in a workspace of n*M uint2 (workgroup (c, m) owns
+// entries m*n + [r0, r1): pairs from the front, full items from the back).
 #include "pq_internal.h"
 
 #include <math.h>
@@ -38,9 +44,12 @@ typedef _Float16 half8 __attribute__((ext_vector_type(8)));
 typedef _Float16 half2v __attribute__((ext_vector_type(2)));
 typedef float float2v __attribute__((ext_vector_type(2)));
 typedef float floatx16 __attribute__((ext_vector_type(16)));
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
 
-constexpr int kWaves = 8;  // 512 threads, 2 waves per SIMD
+constexpr int kWaves = 12;  // 768 threads, 3 waves per SIMD
 constexpr int kThreads = kWaves * 64;
+constexpr int kRsrcWord3 = 0x00020000;  // gfx9 buffer resource: 32-bit data format
 
 // Keeps the three largest of a stream of packed scores.  Inline asm because the compiler
 // quiets every packed value (v_max_f32 v, v, v) before fmaxf / fmed3 in IEEE mode: the
@@ -75,54 +84,168 @@ __device__ __forceinline__ void lds_fence() {
 }
 
 __device__ __forceinline__ uint32_t cvt2(float a, float b) {
-    const half2v h = __builtin_convertvector((float2v){a, b}, half2v);
-    return __builtin_bit_cast(uint32_t, h);
+    const half2v hv = __builtin_convertvector((float2v){a, b}, half2v);
+    return __builtin_bit_cast(uint32_t, hv);
+}
+
+__device__ __forceinline__ float dot2_self(uint32_t u, float acc) {
+    const half2v hv = __builtin_bit_cast(half2v, u);
+    return __builtin_amdgcn_fdot2(hv, hv, acc, false);
+}
+
+__device__ __forceinline__ uint32_t lds_addr(const void* p) { return (uint32_t)(uintptr_t)p; }
+
+// 8 x reads (stride XS bytes) and the 4 reads of two centroid-pair rows (CS bytes apart),
+// all issued back to back, then one lgkmcnt(0).
+template <int G, int XS, int CS>
+__device__ __forceinline__ void lds_burst(uint32_t xa, uint32_t ca, f32x4 (&xq)[G], f32x4& p0, f32x4& p1, f32x4& q0,
+                                          f32x4& q1) {
+    static_assert(G == 8, "burst shape");
+    asm volatile(
+        "ds_read_b128 %0, %12\n\t"
+        "ds_read_b128 %1, %12 offset:%14\n\t"
+        "ds_read_b128 %2, %12 offset:%15\n\t"
+        "ds_read_b128 %3, %12 offset:%16\n\t"
+        "ds_read_b128 %4, %12 offset:%17\n\t"
+        "ds_read_b128 %5, %12 offset:%18\n\t"
+        "ds_read_b128 %6, %12 offset:%19\n\t"
+        "ds_read_b128 %7, %12 offset:%20\n\t"
+        "ds_read_b128 %8, %13\n\t"
+        "ds_read_b128 %9, %13 offset:16\n\t"
+        "ds_read_b128 %10, %13 offset:%21\n\t"
+        "ds_read_b128 %11, %13 offset:%22\n\t"
+        "s_waitcnt lgkmcnt(0)"
+        : "=v"(xq[0]), "=v"(xq[1]), "=v"(xq[2]), "=v"(xq[3]), "=v"(xq[4]), "=v"(xq[5]), "=v"(xq[6]), "=v"(xq[7]),
+          "=v"(p0), "=v"(p1), "=v"(q0), "=v"(q1)
+        : "v"(xa), "v"(ca), "i"(XS), "i"(2 * XS), "i"(3 * XS), "i"(4 * XS), "i"(5 * XS), "i"(6 * XS), "i"(7 * XS),
+          "i"(CS), "i"(CS + 16)
+        : "memory");
+}
+
+// Load instructions per vb: ceil(32 / RPI), RPI = floor(64 / (dsub/4)) >= floor(16 / KS).
+template <int KS>
+constexpr int max_loads() {
+    return (32 + (16 / KS) - 1) / (16 / KS);
 }
 
 // V: profiling variants (tools/cs_variants.hip), 0 in the library.  Bits drop work and
-// produce wrong codes: 1 the 2-candidate checks, 2 the full scans, 4 the top-3 (max only),
-// 8 the MFMAs, 16 the whole filter, 32 all but the first 32 centroids.
-template <int KS, int V = 0>
-struct CsCtx {
-    static constexpr int HALF = 8 * KS;
-    static constexpr int NC = HALF / 4;  // float4 per lane-half
-    const float* xsub;                   // x + m*dsub + h_begin
-    int64_t d, n, r1;
-    const half8* cimg;
-    const float *c32, *hb, *cnl;
-    float* scratch;
-    uint8_t* codesT;
-    int LDR, dsub, h_begin, nchunk, l, r, h, m;
-    float sigma, wa, wb;
-    uint32_t vmask;
+// produce wrong codes: 1 the resolve kernel, 2 its full scans, 4 its pair checks, 8 its x
+// reads, 16 the whole filter, 32 all but the first 32 centroids of the filter.
+template <int KS, int LAYOUT, int V = 0>
+__global__ __launch_bounds__(kThreads) void pq_encode_cs_kernel(
+    const float* __restrict__ x, int64_t n, int d, int M, int dsub, int64_t rows_per_wg,
+    const float* __restrict__ C, const float* __restrict__ cn, const half8* __restrict__ img,
+    const float* __restrict__ hinit, const float4* __restrict__ bnd, uint8_t* __restrict__ codesT,
+    uint2* __restrict__ items, int2* __restrict__ counts) {
+    constexpr int FR = 8 * KS * 64;
+    constexpr int PITCH = 32 * KS + 16;  // bytes per fp16 tile row (16 B pad: conflict-free reads)
+    constexpr int NIMAX = LAYOUT == 0 ? max_loads<KS>() : 2 * KS;
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    half8* cimg = reinterpret_cast<half8*>(smem);
+    unsigned char* stg_all = smem + FR * 16;
+    float* hb = reinterpret_cast<float*>(stg_all + kWaves * 32 * PITCH);
+    float* cnl = hb + 256;
+    int* ctr = reinterpret_cast<int*>(cnl + 256);  // [0] pairs, [1] full, [2] resolve batches
 
-    __device__ __forceinline__ void load(int64_t vb, float4* dst) const {
-        const int64_t row = vb * 32 + r;
-        const bool ok = row < r1;
-        const float* src = xsub + (ok ? row : 0) * d;
-#pragma unroll
-        for (int i = 0; i < NC; ++i)
-            dst[i] = (ok && i < nchunk) ? *reinterpret_cast<const float4*>(src + 4 * i)
-                                        : make_float4(0.f, 0.f, 0.f, 0.f);
+    const int tid = threadIdx.x;
+    const int w = tid >> 6, l = tid & 63;
+    const int r = l & 31, h = l >> 5;
+    const int m = (int)(blockIdx.x % M);
+    const int64_t r0 = (int64_t)(blockIdx.x / M) * rows_per_wg;
+    const int64_t r1 = min(n, r0 + rows_per_wg);
+    if (r0 >= r1) return;
+    const int nrows = (int)(r1 - r0);
+
+    {  // stage the subspace's fp16 codebook image, norms; zero the tiles (pad columns stay 0)
+        const half8* src = img + (int64_t)m * FR;
+        for (int f = tid; f < FR; f += kThreads) cimg[f] = src[f];
+        uint4* z = reinterpret_cast<uint4*>(stg_all);
+        for (int f = tid; f < kWaves * 32 * PITCH / 16; f += kThreads) z[f] = make_uint4(0u, 0u, 0u, 0u);
+        if (tid < 256) {
+            hb[tid] = hinit[(int64_t)m * 256 + tid];
+            cnl[tid] = cn[(int64_t)m * 256 + tid];
+        }
+        if (tid < 4) ctr[tid] = 0;
     }
+    __syncthreads();
 
-    // Encode vb whose x half-rows are resident in xc; the loads of vb_next go into xn first.
-    __device__ __forceinline__ void step(int64_t vb, const float4* xc, int64_t vb_next, int64_t vb_end,
-                                         float4* xn) const {
+    // ------------------------------------------------------------------ phase 1: stream
+    // Load geometry.  LAYOUT 0: instruction i reads rows rpi*i + [0, rpi), lanes past
+    // rpi*q idle.  LAYOUT P in {1, 3}: the vb's 32*q chunks are read in order, 64 per
+    // instruction, all lanes busy; the lane pattern repeats every P instructions (RP rows),
+    // so P per-lane offsets suffice.
+    const int q = dsub >> 2;                 // 16-B chunks per row
+    constexpr int PER = LAYOUT == 0 ? 1 : LAYOUT;
+    const int rpi = LAYOUT == 0 ? min(32, 64 / q) : 64 * PER / q;  // rows per instruction / period
+    const int ni = LAYOUT == 0 ? (32 + rpi - 1) / rpi : q / 2;
+    int prow[PER], voff[PER], toff[PER];
+    bool lactive = true;
+#pragma unroll
+    for (int sidx = 0; sidx < PER; ++sidx) {
+        const int c = LAYOUT == 0 ? l : 64 * sidx + l;
+        prow[sidx] = c / q;
+        const int col = c - prow[sidx] * q;
+        voff[sidx] = (prow[sidx] * d + 4 * col) * 4;
+        toff[sidx] = prow[sidx] * PITCH + 8 * col;
+    }
+    if (LAYOUT == 0) lactive = l < rpi * q;
+    // buffer over this workgroup's rows of subspace m
+    const __amdgpu_buffer_rsrc_t xr_rsrc = __builtin_amdgcn_make_buffer_rsrc(
+        (void*)(x + r0 * d + (int64_t)m * dsub), 0, (int)(((int64_t)(nrows - 1) * d + dsub) * 4), kRsrcWord3);
+
+    const float4 bm = bnd[m];
+    const float sigma = bm.x;
+    const float2v sig2 = {sigma, sigma};
+    const float xs_eta = 6.1035156e-5f * sqrtf((float)dsub);  // 2^-14 * sqrt(dsub)
+    const uint32_t vmask = opaque_mask();
+    unsigned char* stg = stg_all + w * 32 * PITCH;
+    const int nvb = (nrows + 31) >> 5;
+
+    // first tile row of instruction i (uniform part) and this lane's row within it
+    auto ibase = [&](int i) { return LAYOUT == 0 ? rpi * i : rpi * (i / PER); };
+    // lanes past the instruction's rows, and rows past the workgroup's range, load nothing
+    // (raw-buffer range checks do not cover soffset) and write nothing to the tile
+    auto live = [&](int vb, int i) {
+        const int trow = ibase(i) + prow[i % PER];
+        return i < ni && lactive && trow < 32 && trow < nrows - vb * 32;
+    };
+    auto load = [&](int vb, float4* dst) {
+#pragma unroll
+        for (int i = 0; i < NIMAX; ++i) {
+            if (live(vb, i)) {
+                const int soff = (vb * 32 + ibase(i)) * d * 4;
+                const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(xr_rsrc, voff[i % PER], soff, 0);
+                dst[i] = make_float4(__uint_as_float(v[0]), __uint_as_float(v[1]), __uint_as_float(v[2]),
+                                     __uint_as_float(v[3]));
+            }
+        }
+    };
+
+    float4 xr[NIMAX];
+    int vb = w;
+    if (vb < nvb) load(vb, xr);
+    for (; vb < nvb; vb += kWaves) {
+        // sigma * x -> fp16 -> this wave's tile
+#pragma unroll
+        for (int i = 0; i < NIMAX; ++i) {
+            if (live(vb, i)) {
+                const float2v lo = (float2v){xr[i].x, xr[i].y} * sig2;
+                const float2v hi = (float2v){xr[i].z, xr[i].w} * sig2;
+                *reinterpret_cast<uint2*>(stg + ibase(i) * PITCH + toff[i % PER]) =
+                    make_uint2(cvt2(lo.x, lo.y), cvt2(hi.x, hi.y));
+            }
+        }
+        lds_fence();
         half8 bf[KS];
         float xx = 0.0f;
 #pragma unroll
         for (int ks = 0; ks < KS; ++ks) {
-            const float4 a = xc[2 * ks], b = xc[2 * ks + 1];
-            xx = __builtin_fmaf(a.x, a.x, xx); xx = __builtin_fmaf(a.y, a.y, xx);
-            xx = __builtin_fmaf(a.z, a.z, xx); xx = __builtin_fmaf(a.w, a.w, xx);
-            xx = __builtin_fmaf(b.x, b.x, xx); xx = __builtin_fmaf(b.y, b.y, xx);
-            xx = __builtin_fmaf(b.z, b.z, xx); xx = __builtin_fmaf(b.w, b.w, xx);
-            const uint32_t p0 = cvt2(sigma * a.x, sigma * a.y), p1 = cvt2(sigma * a.z, sigma * a.w);
-            const uint32_t p2 = cvt2(sigma * b.x, sigma * b.y), p3 = cvt2(sigma * b.z, sigma * b.w);
-            bf[ks] = __builtin_bit_cast(half8, make_uint4(p0, p1, p2, p3));
+            bf[ks] = *reinterpret_cast<const half8*>(stg + r * PITCH + h * (16 * KS) + 16 * ks);
+            const u32x4 u = __builtin_bit_cast(u32x4, bf[ks]);
+            xx = dot2_self(u[0], xx); xx = dot2_self(u[1], xx);
+            xx = dot2_self(u[2], xx); xx = dot2_self(u[3], xx);
         }
-        if (vb_next < vb_end) load(vb_next, xn);
+        if (vb + kWaves < nvb) load(vb + kWaves, xr);
         xx += __shfl_xor(xx, 32);
 
         float t1 = -INFINITY, t2 = -INFINITY, t3 = -INFINITY;
@@ -133,17 +256,25 @@ struct CsCtx {
             for (int ks = 0; ks < KS; ++ks) a[ks] = cimg[(cb * KS + ks) * 64 + l];
             floatx16 acc;
 #pragma unroll
-            for (int q = 0; q < 4; ++q) {
-                const float4 hv = *reinterpret_cast<const float4*>(hb + cb * 32 + 8 * q + 4 * h);
-                acc[4 * q + 0] = hv.x; acc[4 * q + 1] = hv.y;
-                acc[4 * q + 2] = hv.z; acc[4 * q + 3] = hv.w;
+            for (int qq = 0; qq < 4; ++qq) {
+                const float4 hv = *reinterpret_cast<const float4*>(hb + cb * 32 + 8 * qq + 4 * h);
+                acc[4 * qq + 0] = hv.x; acc[4 * qq + 1] = hv.y;
+                acc[4 * qq + 2] = hv.z; acc[4 * qq + 3] = hv.w;
             }
 #pragma unroll
-            for (int ks = 0; ks < ((V & 8) ? 0 : KS); ++ks) acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(a[ks], bf[ks], acc, 0, 0, 0);
+            for (int ks = 0; ks < KS; ++ks) acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(a[ks], bf[ks], acc, 0, 0, 0);
 #pragma unroll
             for (int i = 0; i < 16; ++i)
-                if constexpr ((V & 4) != 0) asm("v_max_f32 %0, %0, %1" : "+v"(t1) : "v"(pack_idx(acc[i], vmask, (uint32_t)(cb * 32 + (i & 3) + 8 * (i >> 2)))));
-                else top3_insert(t1, t2, t3, pack_idx(acc[i], vmask, (uint32_t)(cb * 32 + (i & 3) + 8 * (i >> 2))));
+                top3_insert(t1, t2, t3, pack_idx(acc[i], vmask, (uint32_t)(cb * 32 + (i & 3) + 8 * (i >> 2))));
+        }
+        if constexpr ((V & 16) != 0) {  // keep the loads and conversions alive
+            uint32_t zz = 0;
+#pragma unroll
+            for (int ks = 0; ks < KS; ++ks) {
+                const u32x4 u = __builtin_bit_cast(u32x4, bf[ks]);
+                zz ^= u[0] ^ u[1] ^ u[2] ^ u[3];
+            }
+            t1 = __uint_as_float(zz & 0x3F0000FFu);
         }
         const uint32_t hbit = (uint32_t)h << 2;
         t1 = __uint_as_float(__float_as_uint(t1) | hbit);
@@ -155,177 +286,255 @@ struct CsCtx {
             top3_insert(t1, t2, t3, p2);
             top3_insert(t1, t2, t3, p3);
         }
-        const float Xs = sigma * sqrtf(xx) * (1.0f + 1e-5f);
-        const float W = wa * Xs + wb;
+        // Xs >= ||sigma x||: |sigma x - x~| <= 2^-11 |sigma x| + 2^-14 per component
+        const float Xs = (sqrtf(xx) * (1.0f + 1e-5f) + xs_eta) * (1.0f + 9.765625e-4f);
+        const float W = bm.y * Xs + bm.z;
         const float thr = t1 - W;
-        const bool bad = !(Xs < 65000.0f) || !(Xs > 1e-12f) || !isfinite(t1) || !isfinite(W);
+        const bool bad = !(Xs < 65000.0f) || !isfinite(t1) || !isfinite(W);
         const int ncand = bad ? 3 : 1 + (t2 >= thr) + (t3 >= thr);
         const int k1 = (int)(__float_as_uint(t1) & 0xFFu);
         const int k2 = (int)(__float_as_uint(t2) & 0xFFu);
-        int code = k1;
-        if constexpr ((V & 16) != 0) {  // keep the loads and conversions alive
-            uint32_t z = 0;
-#pragma unroll
-            for (int ks = 0; ks < KS; ++ks) {
-                const uint4 u = __builtin_bit_cast(uint4, bf[ks]);
-                z ^= u.x ^ u.y ^ u.z ^ u.w;
+        const int rowl = vb * 32 + r;
+        const bool mine = (h == 0) && rowl < nrows;
+        if (mine && ncand == 1) codesT[(int64_t)m * n + r0 + rowl] = (uint8_t)k1;
+        const uint64_t bp = __ballot(mine && ncand == 2);
+        const uint64_t bfull = __ballot(mine && ncand >= 3);
+        if (bp | bfull) {
+            int basep = 0, basef = 0;
+            if (l == 0) {
+                if (bp) basep = atomicAdd(&ctr[0], __popcll(bp));
+                if (bfull) basef = atomicAdd(&ctr[1], __popcll(bfull));
             }
-            code ^= (int)(z & 0xFF);
-        }
-        if (!(V & 1) && __any(ncand == 2)) {
-            const bool need = (ncand == 2);
-            float carry = 0.0f, dot1 = 0.0f, dot2 = 0.0f;
-#pragma unroll
-            for (int phase = 0; phase < 3; ++phase) {
-                // h0: k1 first half, then k2 first half; h1: k1 second half, then k2's
-                const bool active = need && ((h == 0 && phase < 2) || (h == 1 && phase > 0));
-                const int kk = (h == 0) ? (phase == 0 ? k1 : k2) : (phase == 1 ? k1 : k2);
-                float acc = (h == 0) ? 0.0f : carry;
-                if (active) {
-                    const float* crow = c32 + kk * LDR + h_begin;
-#pragma unroll
-                    for (int i = 0; i < NC; ++i) {
-                        if (i < nchunk) {
-                            const float4 cv = *reinterpret_cast<const float4*>(crow + 4 * i);
-                            acc = __builtin_fmaf(xc[i].x, cv.x, acc);
-                            acc = __builtin_fmaf(xc[i].y, cv.y, acc);
-                            acc = __builtin_fmaf(xc[i].z, cv.z, acc);
-                            acc = __builtin_fmaf(xc[i].w, cv.w, acc);
-                        }
-                    }
-                }
-                const float other = __shfl_xor(acc, 32);
-                if (h == 1) {
-                    carry = other;
-                    if (phase == 1) dot1 = acc;
-                    if (phase == 2) dot2 = acc;
-                }
-            }
-            if (need && h == 1) {
-                const float s1 = __builtin_fmaf(-2.0f, dot1, cnl[k1]);
-                const float s2 = __builtin_fmaf(-2.0f, dot2, cnl[k2]);
-                code = (s2 < s1 || (s2 == s1 && k2 < k1)) ? k2 : k1;
-            }
-            code = __shfl(code, (l & 31) + 32);
-        }
-        unsigned long long full = (V & 2) ? 0ull : __ballot(ncand >= 3 && h == 0);
-        while (full) {
-            const int rr = __builtin_ctzll(full);
-            full &= full - 1;
-            if (r == rr) {
-#pragma unroll
-                for (int i = 0; i < NC; ++i) *reinterpret_cast<float4*>(scratch + h_begin + 4 * i) = xc[i];
-            }
-            lds_fence();
-            float acc4[4] = {0.f, 0.f, 0.f, 0.f};
-            for (int t = 0; t < dsub; t += 4) {
-                const float4 xv = *reinterpret_cast<const float4*>(scratch + t);
-#pragma unroll
-                for (int j = 0; j < 4; ++j) {
-                    const float4 cv = *reinterpret_cast<const float4*>(c32 + (l + 64 * j) * LDR + t);
-                    acc4[j] = __builtin_fmaf(xv.x, cv.x, acc4[j]);
-                    acc4[j] = __builtin_fmaf(xv.y, cv.y, acc4[j]);
-                    acc4[j] = __builtin_fmaf(xv.z, cv.z, acc4[j]);
-                    acc4[j] = __builtin_fmaf(xv.w, cv.w, acc4[j]);
-                }
-            }
-            float bs = INFINITY;
-            int bk = l;
-#pragma unroll
-            for (int j = 0; j < 4; ++j) {
-                const float s = __builtin_fmaf(-2.0f, acc4[j], cnl[l + 64 * j]);
-                if (s < bs) { bs = s; bk = l + 64 * j; }
-            }
-#pragma unroll
-            for (int o = 32; o > 0; o >>= 1) {
-                const float os = __shfl_xor(bs, o);
-                const int ok = __shfl_xor(bk, o);
-                if (os < bs || (os == bs && ok < bk)) { bs = os; bk = ok; }
-            }
-            if (r == rr) code = (bs < INFINITY) ? bk : 0;
-            lds_fence();
-        }
-        if (h == 0) {
-            const int64_t row = vb * 32 + r;
-            if (row < r1) codesT[(int64_t)m * n + row] = (uint8_t)code;
+            basep = __shfl(basep, 0);
+            basef = __shfl(basef, 0);
+            const uint64_t below = (1ull << l) - 1ull;
+            uint2* list = items + (int64_t)m * n + r0;
+            if (mine && ncand == 2)
+                list[basep + __popcll(bp & below)] = make_uint2((uint32_t)rowl, (uint32_t)(k1 | (k2 << 8)));
+            if (mine && ncand >= 3) list[nrows - 1 - (basef + __popcll(bfull & below))] = make_uint2((uint32_t)rowl, 0u);
         }
     }
-};
+    __syncthreads();
+    if (tid == 0) counts[blockIdx.x] = make_int2(ctr[0], ctr[1]);
+}
+
+// Resolve: settles the lists of one encode workgroup (same blockIdx -> (chunk, m) mapping).
+// LDS: the exact fp32 C_m with centroid pairs (kp, kp+128) interleaved and zero-padded to
+// 16*KS dimensions (the chains run over the padding without guards: fmaf(0, 0, acc) leaves
+// acc's value unchanged), the norms, and a 16-row x staging tile per wave.  Each wave takes
+// batches of 64 items of one kind; their x sub-rows are gathered 16 at a time with loads
+// whose wave-instruction covers 2-3 whole sub-rows.  A pair item runs on one lane (the
+// canonical fmaf chains of its two candidates); a full item is scanned by the whole wave,
+// four centroids per lane as two v_pk_fma_f32 chains, then an (s, k) minimum across lanes.
+constexpr int kRWaves = 8;
+
+template <int KS>
+constexpr int resolve_smem_bytes() {
+    return 128 * (2 * 16 * KS + 4) * 4 + 256 * 4 + kRWaves * 16 * (16 * KS + 4) * 4 + 16;
+}
 
 template <int KS, int V = 0>
-__global__ __launch_bounds__(kThreads, 2) void pq_encode_cs_kernel(
+__global__ __launch_bounds__(kRWaves * 64) void pq_resolve_cs_kernel(
     const float* __restrict__ x, int64_t n, int d, int M, int dsub, int64_t rows_per_wg,
-    const float* __restrict__ C, const float* __restrict__ cn, const half8* __restrict__ img,
-    const float* __restrict__ hinit, const float4* __restrict__ bnd, uint8_t* __restrict__ codesT) {
-    constexpr int FR = 8 * KS * 64;
-    constexpr int HALF = 8 * KS;
-    constexpr int NC = HALF / 4;
+    const float* __restrict__ C, const float* __restrict__ cn, uint8_t* __restrict__ codesT,
+    const uint2* __restrict__ items, const int2* __restrict__ counts) {
+    constexpr int DP = 16 * KS;
+    constexpr int PP = 2 * DP + 4;  // floats per centroid-pair row
+    constexpr int SP = DP + 4;      // floats per staged x row
+    constexpr int NX = DP / 4;      // float4 per padded sub-row
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-    const int LDR = dsub + 4;
-    half8* cimg = reinterpret_cast<half8*>(smem);
-    float* c32 = reinterpret_cast<float*>(smem + FR * 16);
-    float* hb = c32 + 256 * LDR;
-    float* cnl = hb + 256;
-    float* xsc = cnl + 256;
+    float* cp = reinterpret_cast<float*>(smem);
+    float* cnl = cp + 128 * PP;
+    float* stg_all = cnl + 256;
+    int* ctr = reinterpret_cast<int*>(stg_all + kRWaves * 16 * SP);
 
     const int tid = threadIdx.x;
-    const int w = tid >> 6;
+    const int w = tid >> 6, l = tid & 63;
     const int m = (int)(blockIdx.x % M);
     const int64_t r0 = (int64_t)(blockIdx.x / M) * rows_per_wg;
     const int64_t r1 = min(n, r0 + rows_per_wg);
     if (r0 >= r1) return;
+    const int nrows = (int)(r1 - r0);
+    const int2 cnt = counts[blockIdx.x];
+    const int np = cnt.x, nf = cnt.y;
+    if (np + nf == 0) return;
 
-    {  // stage the subspace's codebook once per workgroup
-        const half8* src = img + (int64_t)m * FR;
-        for (int f = tid; f < FR; f += kThreads) cimg[f] = src[f];
+    {
         const float* Cm = C + (int64_t)m * 256 * dsub;
-        const int q4 = dsub >> 2;
-        for (int e = tid; e < 256 * q4; e += kThreads) {
-            const int k = e / q4, q = e % q4;
-            *reinterpret_cast<float4*>(c32 + k * LDR + 4 * q) =
-                *reinterpret_cast<const float4*>(Cm + (int64_t)k * dsub + 4 * q);
+        for (int e = tid; e < 128 * DP; e += kRWaves * 64) {
+            const int kp = e / DP, t = e - kp * DP;
+            const bool in = t < dsub;
+            *reinterpret_cast<float2*>(cp + kp * PP + 2 * t) =
+                make_float2(in ? Cm[(int64_t)kp * dsub + t] : 0.0f, in ? Cm[(int64_t)(kp + 128) * dsub + t] : 0.0f);
         }
-        if (tid < 256) {
-            hb[tid] = hinit[(int64_t)m * 256 + tid];
-            cnl[tid] = cn[(int64_t)m * 256 + tid];
-        }
+        if (tid < 256) cnl[tid] = cn[(int64_t)m * 256 + tid];
+        if (tid == 0) ctr[0] = 0;
     }
     __syncthreads();
 
-    CsCtx<KS, V> c;
-    c.l = tid & 63;
-    c.r = c.l & 31;
-    c.h = c.l >> 5;
-    c.m = m;
-    c.d = d;
-    c.n = n;
-    c.r1 = r1;
-    c.dsub = dsub;
-    c.LDR = LDR;
-    c.h_begin = c.h * HALF;
-    c.nchunk = max(0, min(HALF, dsub - c.h_begin)) >> 2;
-    c.xsub = x + (int64_t)m * dsub + c.h_begin;
-    c.cimg = cimg;
-    c.c32 = c32;
-    c.hb = hb;
-    c.cnl = cnl;
-    c.scratch = xsc + w * 2 * HALF;
-    c.codesT = codesT;
-    const float4 bm = bnd[m];
-    c.sigma = bm.x;
-    c.wa = bm.y;
-    c.wb = bm.z;
-    c.vmask = opaque_mask();
+    const int q = dsub >> 2;
+    const int nld = (16 * q + 63) >> 6;  // load instructions per 16 staged rows
+    // batches: the heavy full items first (16 per batch, for balance), then pairs (64)
+    const int nbf = (nf + 15) >> 4, nbp = (np + 63) >> 6;
+    const uint2* list = items + (int64_t)m * n + r0;
+    const float* xsub = x + r0 * d + (int64_t)m * dsub;
+    float* stg = stg_all + w * 16 * SP;
+    // Stage sub-rows of items [first + 16*pc, +16) (row offsets in rowl of lanes 16*pc..) into
+    // the tile; loads of a piece are issued one piece ahead, each wave-instruction covering
+    // 2-3 whole sub-rows.
+    auto issue = [&](int pc, int cntb, int rowl, f32x4 (&dst)[KS]) __attribute__((always_inline)) {
+#pragma unroll
+        for (int j = 0; j < KS; ++j) {
+            const int c = j * 64 + l;
+            const int ir = c / q, ch = c - ir * q;
+            const int src = __shfl(rowl, min(pc * 16 + ir, 63));
+            // lanes without a chunk load a harmless in-range address (row 0) instead of branching
+            const bool ok = j < nld && ir < 16 && pc * 16 + ir < cntb;
+            dst[j] = *reinterpret_cast<const f32x4*>(xsub + (ok ? (int64_t)src * d + 4 * ch : 0));
+        }
+    };
+    auto stage = [&](int pc, int cntb, const f32x4 (&src)[KS]) __attribute__((always_inline)) {
+#pragma unroll
+        for (int j = 0; j < KS; ++j) {
+            const int c = j * 64 + l;
+            const int ir = c / q, ch = c - ir * q;
+            if (j < nld && ir < 16 && pc * 16 + ir < cntb)
+                *reinterpret_cast<f32x4*>(stg + ir * SP + 4 * ch) = src[j];
+        }
+        lds_fence();
+    };
 
-    const int64_t vb_end = (r1 + 31) / 32;
-    int64_t vb = r0 / 32 + w;
-    float4 xa[NC], xb[NC];
-    if (vb < vb_end) c.load(vb, xa);
-    // two vbs per trip so that the prefetch target alternates between xa and xb
-    for (; vb < vb_end; vb += 2 * kWaves) {
-        c.step(vb, xa, vb + kWaves, vb_end, xb);
-        if (vb + kWaves >= vb_end) break;
-        c.step(vb + kWaves, xb, vb + 2 * kWaves, vb_end, xa);
+    for (;;) {
+        int b = 0;
+        if (l == 0) b = atomicAdd(&ctr[0], 1);
+        b = __shfl(b, 0);
+        if (b >= nbp + nbf) break;
+        f32x4 ga[KS], gb[KS];
+        if (b < nbf) {
+            // ---- 16 full items: the wave scans G staged rows at a time, lane l taking the
+            // centroid pairs (l, l+128) and (l+64, l+192) of each: 2G independent
+            // v_pk_fma_f32 chains, and each centroid read serves G rows
+            const int first = b * 16;
+            const int cntb = min(16, nf - first);
+            int rowl = 0;
+            if (l < cntb) rowl = (int)list[nrows - 1 - (first + l)].x;
+            issue(0, cntb, rowl, ga);
+            stage(0, cntb, ga);
+            if constexpr ((V & 10) != 0) { lds_fence(); continue; }
+            constexpr int G = 8;
+            const float* ca = cp + l * PP;
+            const float* cb = cp + (l + 64) * PP;
+            for (int g0 = 0; g0 < cntb; g0 += G) {
+                float2v a[G], bb[G];
+#pragma unroll
+                for (int g = 0; g < G; ++g) a[g] = bb[g] = (float2v){0.0f, 0.0f};
+                const float* xg = stg + g0 * SP;  // rows past cntb hold stale data: unused
+                const uint32_t xa0 = lds_addr(xg), ca0 = lds_addr(ca);
+#pragma unroll 1
+                for (int i = 0; i < q; ++i) {
+                    // the G x vectors and 4 centroid-pair vectors of step i in one burst, one wait
+                    // (left to itself the compiler issues and waits for the x reads one by one)
+                    f32x4 xq[G], p0, p1, q0, q1;
+                    lds_burst<G, SP * 4, 64 * PP * 4>(xa0 + 16 * i, ca0 + 32 * i, xq, p0, p1, q0, q1);
+#pragma unroll
+                    for (int g = 0; g < G; ++g) {
+                        a[g] = __builtin_elementwise_fma((float2v){xq[g].x, xq[g].x}, (float2v){p0.x, p0.y}, a[g]);
+                        bb[g] = __builtin_elementwise_fma((float2v){xq[g].x, xq[g].x}, (float2v){q0.x, q0.y}, bb[g]);
+                        a[g] = __builtin_elementwise_fma((float2v){xq[g].y, xq[g].y}, (float2v){p0.z, p0.w}, a[g]);
+                        bb[g] = __builtin_elementwise_fma((float2v){xq[g].y, xq[g].y}, (float2v){q0.z, q0.w}, bb[g]);
+                        a[g] = __builtin_elementwise_fma((float2v){xq[g].z, xq[g].z}, (float2v){p1.x, p1.y}, a[g]);
+                        bb[g] = __builtin_elementwise_fma((float2v){xq[g].z, xq[g].z}, (float2v){q1.x, q1.y}, bb[g]);
+                        a[g] = __builtin_elementwise_fma((float2v){xq[g].w, xq[g].w}, (float2v){p1.z, p1.w}, a[g]);
+                        bb[g] = __builtin_elementwise_fma((float2v){xq[g].w, xq[g].w}, (float2v){q1.z, q1.w}, bb[g]);
+                    }
+                }
+                // per row: this lane's 4 centroids in increasing k, then the (s, k) minimum
+                // across lanes (NaN never wins; all-NaN/inf rows give 0)
+                float bs[G];
+                int bk[G];
+#pragma unroll
+                for (int g = 0; g < G; ++g) {
+                    bs[g] = INFINITY;
+                    bk[g] = l;
+                    const float s0 = __builtin_fmaf(-2.0f, a[g].x, cnl[l]);
+                    const float s1 = __builtin_fmaf(-2.0f, bb[g].x, cnl[l + 64]);
+                    const float s2 = __builtin_fmaf(-2.0f, a[g].y, cnl[l + 128]);
+                    const float s3 = __builtin_fmaf(-2.0f, bb[g].y, cnl[l + 192]);
+                    if (s0 < bs[g]) { bs[g] = s0; bk[g] = l; }
+                    if (s1 < bs[g]) { bs[g] = s1; bk[g] = l + 64; }
+                    if (s2 < bs[g]) { bs[g] = s2; bk[g] = l + 128; }
+                    if (s3 < bs[g]) { bs[g] = s3; bk[g] = l + 192; }
+                }
+#pragma unroll
+                for (int o = 32; o > 0; o >>= 1) {
+#pragma unroll
+                    for (int g = 0; g < G; ++g) {
+                        const float os = __shfl_xor(bs[g], o);
+                        const int ok = __shfl_xor(bk[g], o);
+                        if (os < bs[g] || (os == bs[g] && ok < bk[g])) { bs[g] = os; bk[g] = ok; }
+                    }
+                }
+#pragma unroll
+                for (int g = 0; g < G; ++g) {
+                    const int rw = __shfl(rowl, min(g0 + g, 63));
+                    if (l == 0 && g0 + g < cntb)
+                        codesT[(int64_t)m * n + r0 + rw] = (uint8_t)((bs[g] < INFINITY) ? bk[g] : 0);
+                }
+            }
+            lds_fence();
+        } else {
+            // ---- 64 pairs, one per lane: the canonical chains of its two candidates
+            const int first = (b - nbf) * 64;
+            const int cntb = min(64, np - first);
+            const bool live = l < cntb;
+            uint2 it = make_uint2(0u, 0u);
+            if (live) it = list[first + l];
+            const int rowl = (int)it.x;
+            float4 xv[NX];
+#pragma unroll
+            for (int i = 0; i < NX; ++i) xv[i] = make_float4(0.f, 0.f, 0.f, 0.f);
+            // the lanes of piece pc copy their staged row; pieces alternate between two
+            // register buffers so that the next piece's loads are always in flight
+            auto take = [&](int pc) __attribute__((always_inline)) {
+                if ((l >> 4) == pc && live) {
+                    const float* xr = stg + (l & 15) * SP;
+#pragma unroll
+                    for (int i = 0; i < NX; ++i)
+                        if (4 * i < dsub) xv[i] = *reinterpret_cast<const float4*>(xr + 4 * i);
+                }
+                lds_fence();
+            };
+            issue(0, cntb, rowl, ga);
+            if (cntb > 16) issue(1, cntb, rowl, gb);
+            stage(0, cntb, ga);
+            take(0);
+            if (cntb > 32) issue(2, cntb, rowl, ga);
+            if (cntb > 16) { stage(1, cntb, gb); take(1); }
+            if (cntb > 48) issue(3, cntb, rowl, gb);
+            if (cntb > 32) { stage(2, cntb, ga); take(2); }
+            if (cntb > 48) { stage(3, cntb, gb); take(3); }
+            if (!live) continue;
+            if constexpr ((V & 12) != 0) continue;
+            const int k1 = (int)(it.y & 0xFFu), k2 = (int)((it.y >> 8) & 0xFFu);
+            const float* c1 = cp + (k1 & 127) * PP + (k1 >> 7);
+            const float* c2 = cp + (k2 & 127) * PP + (k2 >> 7);
+            float d1 = 0.0f, d2 = 0.0f;
+#pragma unroll
+            for (int i = 0; i < NX; ++i) {
+                const int t = 4 * i;
+                d1 = __builtin_fmaf(xv[i].x, c1[2 * t + 0], d1);
+                d2 = __builtin_fmaf(xv[i].x, c2[2 * t + 0], d2);
+                d1 = __builtin_fmaf(xv[i].y, c1[2 * t + 2], d1);
+                d2 = __builtin_fmaf(xv[i].y, c2[2 * t + 2], d2);
+                d1 = __builtin_fmaf(xv[i].z, c1[2 * t + 4], d1);
+                d2 = __builtin_fmaf(xv[i].z, c2[2 * t + 4], d2);
+                d1 = __builtin_fmaf(xv[i].w, c1[2 * t + 6], d1);
+                d2 = __builtin_fmaf(xv[i].w, c2[2 * t + 6], d2);
+            }
+            const float s1 = __builtin_fmaf(-2.0f, d1, cnl[k1]);
+            const float s2 = __builtin_fmaf(-2.0f, d2, cnl[k2]);
+            codesT[(int64_t)m * n + r0 + rowl] = (uint8_t)((s2 < s1 || (s2 == s1 && k2 < k1)) ? k2 : k1);
+        }
     }
 }
 
@@ -351,52 +560,77 @@ int device_cus() {
 }
 
 // Chunk count for one workgroup per CU at a time: minimise the rounds of workgroups per row
-// (ceil(chunks*M / CUs) / chunks), preferring fewer chunks, with at least 32*kWaves rows each.
-int64_t pick_chunks(int64_t n, int M, int cus) {
-    const int64_t cmax = std::max<int64_t>(1, std::min<int64_t>(ceil_div(n, 32 * kWaves), 4 * (int64_t)cus));
-    int64_t best = 1;
+// (ceil(chunks*M / CUs) / chunks), preferring fewer chunks, with at least 32*kWaves rows each
+// and few enough rows that a chunk's buffer offsets fit 31 bits.
+int64_t pick_chunks(int64_t n, int d, int M, int cus) {
+    const int64_t rmax = std::max<int64_t>(32, ((int64_t)1 << 31) / ((int64_t)d * 4) - 64);
+    const int64_t cmin = ceil_div(n, rmax);
+    const int64_t cmax = std::max<int64_t>(cmin, std::min<int64_t>(ceil_div(n, 32 * kWaves), 4 * (int64_t)cus));
+    int64_t best = cmin;
     double best_cost = 1e300;
-    for (int64_t c = 1; c <= cmax; ++c) {
+    for (int64_t c = cmin; c <= cmax; ++c) {
         const double cost = (double)ceil_div(c * M, (int64_t)cus) / (double)c;
         if (cost < best_cost * (1.0 - 1e-9)) { best_cost = cost; best = c; }
     }
     return best;
 }
 
-template <int KS, int V = 0>
-hipError_t launch_ks(const float* x, int64_t n, int d, int M, int dsub, const float* C, const float* cn,
-                     const void* img, const float* hinit, const void* bnd, uint8_t* codesT, hipStream_t st) {
-    const int smem = cs_smem_bytes(KS, dsub);
-    auto kern = pq_encode_cs_kernel<KS, V>;
-    hipError_t e = hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, smem);
-    if (e != hipSuccess) return e;
-    static thread_local int cus = 0;
-    if (!cus) cus = device_cus();
-    const int64_t chunks = pick_chunks(n, M, cus);
-    const int64_t R = align_up(ceil_div(n, chunks), (int64_t)32);
-    const int64_t grid = ceil_div(n, R) * M;
-    hipLaunchKernelGGL(kern, dim3((unsigned)grid), dim3(kThreads), smem, st, x, n, d, M, dsub, R, C, cn,
-                       static_cast<const half8*>(img), hinit, static_cast<const float4*>(bnd), codesT);
-    return hipGetLastError();
-}
-
 }  // namespace
 
 int cs_smem_bytes(int KS, int dsub) {
-    return 8 * KS * 64 * 16 + 256 * (dsub + 4) * 4 + 2 * 256 * 4 + kWaves * 2 * 8 * KS * 4;
+    (void)dsub;
+    return 8 * KS * 64 * 16 + kWaves * 32 * (32 * KS + 16) + 2 * 256 * 4 + 16;
 }
+
+// Load layout for dsub (see the kernel): period-P flat layouts where all lanes stay busy.
+int cs_layout(int dsub) {
+    switch (dsub >> 2) {
+        case 2: case 4: case 8: case 16: return 1;
+        case 6: case 12: case 24: return 3;
+        default: return 0;
+    }
+}
+
+template <int KS, int V>
+hipError_t launch_pq_encode_cs_v(const float* x, int64_t n, int d, int M, int dsub, const float* C, const float* cn,
+                                 const void* img, const float* hinit, const void* bnd, uint8_t* codesT, void* items,
+                                 void* counts, hipStream_t st) {
+    const int smem = cs_smem_bytes(KS, dsub);
+    const int layout = cs_layout(dsub);
+    auto kern = layout == 1 ? pq_encode_cs_kernel<KS, 1, V>
+              : layout == 3 ? pq_encode_cs_kernel<KS, 3, V> : pq_encode_cs_kernel<KS, 0, V>;
+    hipError_t e = hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, smem);
+    if (e != hipSuccess) return e;
+    constexpr int rsmem = resolve_smem_bytes<KS>();
+    auto rkern = pq_resolve_cs_kernel<KS, V>;
+    e = hipFuncSetAttribute((const void*)rkern, hipFuncAttributeMaxDynamicSharedMemorySize, rsmem);
+    if (e != hipSuccess) return e;
+    static thread_local int cus = 0;
+    if (!cus) cus = device_cus();
+    const int64_t chunks = pick_chunks(n, d, M, cus);
+    const int64_t R = align_up(ceil_div(n, chunks), (int64_t)32);
+    const int64_t grid = ceil_div(n, R) * M;
+    hipLaunchKernelGGL(kern, dim3((unsigned)grid), dim3(kThreads), smem, st, x, n, d, M, dsub, R, C, cn,
+                       static_cast<const half8*>(img), hinit, static_cast<const float4*>(bnd), codesT,
+                       static_cast<uint2*>(items), static_cast<int2*>(counts));
+    e = hipGetLastError();
+    if (e != hipSuccess || (V & 1)) return e;
+    hipLaunchKernelGGL(rkern, dim3((unsigned)grid), dim3(kRWaves * 64), rsmem, st, x, n, d, M, dsub, R, C, cn, codesT,
+                       static_cast<const uint2*>(items), static_cast<const int2*>(counts));
+    return hipGetLastError();
+}
+
+size_t cs_counts_bytes(int64_t n, int M) { return (size_t)ceil_div(n, 32 * kWaves) * M * sizeof(int2); }
 
 hipError_t launch_pq_encode_cs(int KS, const float* x, int64_t n, int d, int M, int dsub, const float* C,
                                const float* cn, const void* img, const float* hinit, const void* bnd,
-                               uint8_t* codesT, uint8_t* codes, hipStream_t st) {
+                               uint8_t* codesT, void* items, void* counts, uint8_t* codes, hipStream_t st) {
     hipError_t e = hipErrorInvalidValue;
     switch (KS) {
-        case 1: e = launch_ks<1>(x, n, d, M, dsub, C, cn, img, hinit, bnd, codesT, st); break;
-        case 2: e = launch_ks<2>(x, n, d, M, dsub, C, cn, img, hinit, bnd, codesT, st); break;
-        case 3: e = launch_ks<3>(x, n, d, M, dsub, C, cn, img, hinit, bnd, codesT, st); break;
-        case 4: e = launch_ks<4>(x, n, d, M, dsub, C, cn, img, hinit, bnd, codesT, st); break;
-        case 5: e = launch_ks<5>(x, n, d, M, dsub, C, cn, img, hinit, bnd, codesT, st); break;
-        case 6: e = launch_ks<6>(x, n, d, M, dsub, C, cn, img, hinit, bnd, codesT, st); break;
+#define MIVQ_CS_CASE(k)                                                                                        \
+    case k: e = launch_pq_encode_cs_v<k, 0>(x, n, d, M, dsub, C, cn, img, hinit, bnd, codesT, items, counts, st); break;
+        MIVQ_CS_CASE(1) MIVQ_CS_CASE(2) MIVQ_CS_CASE(3) MIVQ_CS_CASE(4) MIVQ_CS_CASE(5) MIVQ_CS_CASE(6)
+#undef MIVQ_CS_CASE
         default: return hipErrorInvalidValue;
     }
     if (e != hipSuccess) return e;

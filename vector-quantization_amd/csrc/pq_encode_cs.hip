@@ -122,6 +122,22 @@ __device__ __forceinline__ void lds_burst(uint32_t xa, uint32_t ca, f32x4 (&xq)[
         : "memory");
 }
 
+// Workgroup -> (subspace m, row chunk).  Workgroups are dealt to the 8 XCDs round-robin; when
+// the grid allows, each XCD gets all M subspaces of a chunk in consecutive slots, so the M
+// workgroups reading one row range run side by side on one XCD and sweep the same DRAM pages
+// together.  Both kernels of the encode use the same mapping (the lists are per workgroup).
+__device__ __forceinline__ void wg_coords(int M, int& m, int64_t& chunk) {
+    const unsigned b = blockIdx.x, g = gridDim.x;
+    if (g % (8u * (unsigned)M) == 0) {
+        const unsigned j = b >> 3;
+        m = (int)(j % (unsigned)M);
+        chunk = (int64_t)(j / (unsigned)M) * 8 + (b & 7u);
+    } else {
+        m = (int)(b % (unsigned)M);
+        chunk = b / (unsigned)M;
+    }
+}
+
 // Load instructions per vb: ceil(32 / RPI), RPI = floor(64 / (dsub/4)) >= floor(16 / KS).
 template <int KS>
 constexpr int max_loads() {
@@ -130,7 +146,8 @@ constexpr int max_loads() {
 
 // V: profiling variants (tools/cs_variants.hip), 0 in the library.  Bits drop work and
 // produce wrong codes: 1 the resolve kernel, 2 its full scans, 4 its pair checks, 8 its x
-// reads, 16 the whole filter, 32 all but the first 32 centroids of the filter.
+// reads, 16 the whole filter, 32 all but the first 32 centroids of the filter, 64 the x
+// loads after a wave's second vb (compute alone).
 template <int KS, int LAYOUT, int V = 0>
 __global__ __launch_bounds__(kThreads) void pq_encode_cs_kernel(
     const float* __restrict__ x, int64_t n, int d, int M, int dsub, int64_t rows_per_wg,
@@ -148,10 +165,12 @@ __global__ __launch_bounds__(kThreads) void pq_encode_cs_kernel(
     int* ctr = reinterpret_cast<int*>(cnl + 256);  // [0] pairs, [1] full, [2] resolve batches
 
     const int tid = threadIdx.x;
-    const int w = tid >> 6, l = tid & 63;
+    const int w = __builtin_amdgcn_readfirstlane(tid >> 6), l = tid & 63;  // w: wave-uniform (SGPR)
     const int r = l & 31, h = l >> 5;
-    const int m = (int)(blockIdx.x % M);
-    const int64_t r0 = (int64_t)(blockIdx.x / M) * rows_per_wg;
+    int m;
+    int64_t chunk;
+    wg_coords(M, m, chunk);
+    const int64_t r0 = chunk * rows_per_wg;
     const int64_t r1 = min(n, r0 + rows_per_wg);
     if (r0 >= r1) return;
     const int nrows = (int)(r1 - r0);
@@ -209,15 +228,23 @@ __global__ __launch_bounds__(kThreads) void pq_encode_cs_kernel(
         const int trow = ibase(i) + prow[i % PER];
         return i < ni && lactive && trow < 32 && trow < nrows - vb * 32;
     };
+    // a whole vb in a flat layout: every lane of the first ni instructions is live (uniform test)
+    auto whole = [&](int vb) { return LAYOUT != 0 && nrows - vb * 32 >= 32; };
     auto load = [&](int vb, float4* dst) {
+        auto one = [&](int i) __attribute__((always_inline)) {
+            const int soff = (vb * 32 + ibase(i)) * d * 4;
+            const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(xr_rsrc, voff[i % PER], soff, 0);
+            dst[i] = make_float4(__uint_as_float(v[0]), __uint_as_float(v[1]), __uint_as_float(v[2]),
+                                 __uint_as_float(v[3]));
+        };
+        if (whole(vb)) {
 #pragma unroll
-        for (int i = 0; i < NIMAX; ++i) {
-            if (live(vb, i)) {
-                const int soff = (vb * 32 + ibase(i)) * d * 4;
-                const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(xr_rsrc, voff[i % PER], soff, 0);
-                dst[i] = make_float4(__uint_as_float(v[0]), __uint_as_float(v[1]), __uint_as_float(v[2]),
-                                     __uint_as_float(v[3]));
-            }
+            for (int i = 0; i < NIMAX; ++i)
+                if (i < ni) one(i);
+        } else {
+#pragma unroll
+            for (int i = 0; i < NIMAX; ++i)
+                if (live(vb, i)) one(i);
         }
     };
 
@@ -226,14 +253,19 @@ __global__ __launch_bounds__(kThreads) void pq_encode_cs_kernel(
     if (vb < nvb) load(vb, xr);
     for (; vb < nvb; vb += kWaves) {
         // sigma * x -> fp16 -> this wave's tile
+        auto put = [&](int i) __attribute__((always_inline)) {
+            const float2v lo = (float2v){xr[i].x, xr[i].y} * sig2;
+            const float2v hi = (float2v){xr[i].z, xr[i].w} * sig2;
+            *reinterpret_cast<uint2*>(stg + ibase(i) * PITCH + toff[i % PER]) = make_uint2(cvt2(lo.x, lo.y), cvt2(hi.x, hi.y));
+        };
+        if (whole(vb)) {
 #pragma unroll
-        for (int i = 0; i < NIMAX; ++i) {
-            if (live(vb, i)) {
-                const float2v lo = (float2v){xr[i].x, xr[i].y} * sig2;
-                const float2v hi = (float2v){xr[i].z, xr[i].w} * sig2;
-                *reinterpret_cast<uint2*>(stg + ibase(i) * PITCH + toff[i % PER]) =
-                    make_uint2(cvt2(lo.x, lo.y), cvt2(hi.x, hi.y));
-            }
+            for (int i = 0; i < NIMAX; ++i)
+                if (i < ni) put(i);
+        } else {
+#pragma unroll
+            for (int i = 0; i < NIMAX; ++i)
+                if (live(vb, i)) put(i);
         }
         lds_fence();
         half8 bf[KS];
@@ -245,12 +277,14 @@ __global__ __launch_bounds__(kThreads) void pq_encode_cs_kernel(
             xx = dot2_self(u[0], xx); xx = dot2_self(u[1], xx);
             xx = dot2_self(u[2], xx); xx = dot2_self(u[3], xx);
         }
-        if (vb + kWaves < nvb) load(vb + kWaves, xr);
+        if (vb + kWaves < nvb && !((V & 64) && vb >= kWaves)) load(vb + kWaves, xr);
         xx += __shfl_xor(xx, 32);
 
         float t1 = -INFINITY, t2 = -INFINITY, t3 = -INFINITY;
-#pragma unroll
-        for (int cb = 0; cb < ((V & 16) ? 0 : (V & 32) ? 1 : 8); ++cb) {
+        constexpr int NCB = (V & 16) ? 0 : (V & 32) ? 1 : 8;
+        // MFMAs of centroid block cb+1 go into the other accumulator before the top-3 of cb
+        // reads this one, so a wave's matrix and vector work overlap
+        auto scores = [&](int cb) __attribute__((always_inline)) {
             half8 a[KS];
 #pragma unroll
             for (int ks = 0; ks < KS; ++ks) a[ks] = cimg[(cb * KS + ks) * 64 + l];
@@ -263,9 +297,19 @@ __global__ __launch_bounds__(kThreads) void pq_encode_cs_kernel(
             }
 #pragma unroll
             for (int ks = 0; ks < KS; ++ks) acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(a[ks], bf[ks], acc, 0, 0, 0);
+            return acc;
+        };
+        if constexpr (NCB > 0) {
+            floatx16 acc_cur = scores(0);
 #pragma unroll
-            for (int i = 0; i < 16; ++i)
-                top3_insert(t1, t2, t3, pack_idx(acc[i], vmask, (uint32_t)(cb * 32 + (i & 3) + 8 * (i >> 2))));
+            for (int cb = 0; cb < NCB; ++cb) {
+                floatx16 acc_next;
+                if (cb + 1 < NCB) acc_next = scores(cb + 1);
+#pragma unroll
+                for (int i = 0; i < 16; ++i)
+                    top3_insert(t1, t2, t3, pack_idx(acc_cur[i], vmask, (uint32_t)(cb * 32 + (i & 3) + 8 * (i >> 2))));
+                if (cb + 1 < NCB) acc_cur = acc_next;
+            }
         }
         if constexpr ((V & 16) != 0) {  // keep the loads and conversions alive
             uint32_t zz = 0;
@@ -350,8 +394,10 @@ __global__ __launch_bounds__(kRWaves * 64) void pq_resolve_cs_kernel(
 
     const int tid = threadIdx.x;
     const int w = tid >> 6, l = tid & 63;
-    const int m = (int)(blockIdx.x % M);
-    const int64_t r0 = (int64_t)(blockIdx.x / M) * rows_per_wg;
+    int m;
+    int64_t chunk;
+    wg_coords(M, m, chunk);
+    const int64_t r0 = chunk * rows_per_wg;
     const int64_t r1 = min(n, r0 + rows_per_wg);
     if (r0 >= r1) return;
     const int nrows = (int)(r1 - r0);

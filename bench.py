@@ -3,7 +3,7 @@
 Workload (BASELINE.json configs[1]): PQ M=16 B=8 encode of 1M x 1536 fp32 per GPU
 (weak scaling: every rank owns its own 1M-row shard, generated on its device from seed =
 rank, unit-normalised rows).  One "step" = one encode pass over the resident shard through
-libmivq (mivq_pq_encode: fp16-MFMA filter kernel + exact re-check/resolve kernel).
+libmivq (mivq_pq_encode: fp16-MFMA filter kernel, exact resolve kernel, code transpose).
 Codebooks: rank 0 trains them on its first 65,536 rows (GPU k-means, 25 iterations,
 seed 1234) and broadcasts them (RCCL).  After the timed encode, the ADC leg searches the
 encoded shards for `--nq` queries (broadcast from rank 0; per-shard top-10, RCCL
@@ -144,7 +144,7 @@ def main():
     C = torch.empty((a.M, 256, a.d // a.M), dtype=torch.float32, device=dev)
     if rank == 0:
         t0 = time.perf_counter()
-        C.copy_(train_pq(X[:65536], a.M, nbits, niter=25, seed=1234))
+        C.copy_(train_pq(X[:65536], a.M, nbits, niter=25, seed=1234, exact_assign=True))
         torch.cuda.synchronize()
         log(f"[rank 0] k-means fit on 65536 rows: {time.perf_counter() - t0:.2f} s")
     if world > 1:
@@ -219,7 +219,8 @@ def main():
                        "parallelism": f"row-sharded x{world}"},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic_from_profile(workload),
-                         "kernel": "pq_encode_cs_kernel + pq_transpose_codes_kernel (one mivq_pq_encode call)",
+                         "kernel": "mivq_pq_encode call: pq_encode_cs_kernel (filter) + pq_resolve_cs_kernel "
+                                   "(exact re-check of the rows the filter could not settle) + pq_transpose_codes_kernel",
                          "bytes_per_vector": bytes_per_vec, "kernel_ms": kern_ms},
             "cpu_baseline": cpu,
             "parity_sample": parity,

@@ -51,8 +51,14 @@ def _split_empty(C: np.ndarray, counts: np.ndarray, rng: np.random.Generator, n:
 
 
 def train_pq(X: torch.Tensor, M: int, nbits: int, niter: int = 25, seed: int = 1234,
-             max_points_per_centroid: int = 256, init: torch.Tensor | None = None) -> torch.Tensor:
-    """Train (M, 2**nbits, d/M) f32 centroids on device rows X (n, d)."""
+             max_points_per_centroid: int = 256, init: torch.Tensor | None = None,
+             exact_assign: bool = False) -> torch.Tensor:
+    """Train (M, 2**nbits, d/M) f32 centroids on device rows X (n, d).
+
+    exact_assign: assign with the exact VALU encode instead of the MFMA filter path (same
+    codes, so the same centroids; bench.py uses it to keep its profile free of training
+    launches of the filter kernels).
+    """
     n, d = X.shape
     if d % M != 0:
         raise AssertionError("D must be divisible by M (number of subquantizers)")
@@ -78,7 +84,7 @@ def train_pq(X: torch.Tensor, M: int, nbits: int, niter: int = 25, seed: int = 1
     counts = torch.empty((M, ksub), dtype=torch.int32, device=X.device)
     for _ in range(niter):
         prep = _native.pq_prepare(C, nbits)
-        codes = _native.pq_encode(Xt, C, prep, nbits)
+        codes = _native.pq_encode(Xt, C, prep, nbits, exact=exact_assign)
         assign = codes if nbits == 8 else _native.pq_unpack(codes, M, nbits)
         _native.kmeans_update(Xt, assign, C, counts)
         cnt = counts.cpu().numpy()

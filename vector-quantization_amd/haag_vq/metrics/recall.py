@@ -12,7 +12,7 @@ from haag_vq.methods.search.flat_quantized_index import ids_to_numpy, search_cod
 
 def retrieve(data, model, k: int, num_queries: int = 100) -> np.ndarray:
     queries = np.asarray(data.queries[:num_queries], dtype=np.float32)
-    codes = model.compress(np.asarray(data.vectors, dtype=np.float32))
+    codes = model.compress(data.vectors)  # the dataset's own dtype, as the reference (recall.py:12)
     k = min(k, len(data.vectors))
     _, ids = search_codes(model, codes, queries, k, "l2")
     return ids_to_numpy(ids).astype(np.int64)

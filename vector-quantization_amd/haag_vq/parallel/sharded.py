@@ -52,12 +52,13 @@ def exchange_topk(d: torch.Tensor, i: torch.Tensor, k: int,
     if world == 1:
         return d, i
     nq = d.shape[0]
-    gd = torch.empty((world, nq, k), dtype=d.dtype, device=d.device)
-    gi = torch.empty((world, nq, k), dtype=i.dtype, device=i.device)
+    # output concatenated along dim 0 (the form every backend accepts), viewed per rank
+    gd = torch.empty((world * nq, k), dtype=d.dtype, device=d.device)
+    gi = torch.empty((world * nq, k), dtype=i.dtype, device=i.device)
     dist.all_gather_into_tensor(gd, d.contiguous())
     dist.all_gather_into_tensor(gi, i.contiguous())
     merge = merge or _native.topk_merge
-    return merge(gd, gi, k)
+    return merge(gd.view(world, nq, k), gi.view(world, nq, k), k)
 
 
 def sharded_adc_search(Q: torch.Tensor, C: torch.Tensor, codes_u8: torch.Tensor, nbits: int, k: int,

@@ -21,7 +21,8 @@ from bench import synth  # noqa: E402
 
 VARIANTS = {0: "encode + resolve", 1: "encode only", 2: "resolve: pairs only", 4: "resolve: full scans only",
             8: "resolve: gathers, no compute", 33: "encode only, 1 of 8 cb",
-            17: "loads + convert + tile + fragments only", 65: "encode only, no x loads (compute alone)"}
+            17: "loads + convert + tile + fragments only", 65: "encode only, no x loads (compute alone)",
+            145: "streaming only, subspace-major probe"}
 
 
 def prep_layout(M, dsub, ksub=256):

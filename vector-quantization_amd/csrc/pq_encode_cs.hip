@@ -48,6 +48,7 @@ typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 
 constexpr int kWaves = 12;  // 768 threads, 3 waves per SIMD
+constexpr int kDepth = 1;   // x blocks in flight per wave
 constexpr int kThreads = kWaves * 64;
 constexpr int kRsrcWord3 = 0x00020000;  // gfx9 buffer resource: 32-bit data format
 
@@ -147,7 +148,8 @@ constexpr int max_loads() {
 // V: profiling variants (tools/cs_variants.hip), 0 in the library.  Bits drop work and
 // produce wrong codes: 1 the resolve kernel, 2 its full scans, 4 its pair checks, 8 its x
 // reads, 16 the whole filter, 32 all but the first 32 centroids of the filter, 64 the x
-// loads after a wave's second vb (compute alone).
+// loads after a wave's second vb (compute alone), 128 reads the same bytes as if x were
+// stored subspace-major (contiguous per workgroup: a memory-pattern probe).
 template <int KS, int LAYOUT, int V = 0>
 __global__ __launch_bounds__(kThreads) void pq_encode_cs_kernel(
     const float* __restrict__ x, int64_t n, int d, int M, int dsub, int64_t rows_per_wg,
@@ -194,6 +196,7 @@ __global__ __launch_bounds__(kThreads) void pq_encode_cs_kernel(
     // instruction, all lanes busy; the lane pattern repeats every P instructions (RP rows),
     // so P per-lane offsets suffice.
     const int q = dsub >> 2;                 // 16-B chunks per row
+    const int XS = (V & 128) ? dsub : d;     // row stride of the loads (V&128: subspace-major probe)
     constexpr int PER = LAYOUT == 0 ? 1 : LAYOUT;
     const int rpi = LAYOUT == 0 ? min(32, 64 / q) : 64 * PER / q;  // rows per instruction / period
     const int ni = LAYOUT == 0 ? (32 + rpi - 1) / rpi : q / 2;
@@ -204,13 +207,19 @@ __global__ __launch_bounds__(kThreads) void pq_encode_cs_kernel(
         const int c = LAYOUT == 0 ? l : 64 * sidx + l;
         prow[sidx] = c / q;
         const int col = c - prow[sidx] * q;
-        voff[sidx] = (prow[sidx] * d + 4 * col) * 4;
+        voff[sidx] = (prow[sidx] * XS + 4 * col) * 4;
         toff[sidx] = prow[sidx] * PITCH + 8 * col;
     }
     if (LAYOUT == 0) lactive = l < rpi * q;
-    // buffer over this workgroup's rows of subspace m
+    // Buffer over this workgroup's rows of subspace m.  The whole byte offset goes in the
+    // (range-checked) VGPR offset, so rows past the range read as zeros without a branch;
+    // idle lanes of LAYOUT 0 get an offset >= 2^31, past any range.
     const __amdgpu_buffer_rsrc_t xr_rsrc = __builtin_amdgcn_make_buffer_rsrc(
-        (void*)(x + r0 * d + (int64_t)m * dsub), 0, (int)(((int64_t)(nrows - 1) * d + dsub) * 4), kRsrcWord3);
+        (void*)(x + ((V & 128) ? ((int64_t)m * n + r0) * dsub : r0 * d + (int64_t)m * dsub)), 0,
+        (int)(((int64_t)(nrows - 1) * XS + dsub) * 4), kRsrcWord3);
+#pragma unroll
+    for (int sidx = 0; sidx < PER; ++sidx)
+        if (!lactive) voff[sidx] = (int)0x80000000u;
 
     const float4 bm = bnd[m];
     const float sigma = bm.x;
@@ -222,50 +231,32 @@ __global__ __launch_bounds__(kThreads) void pq_encode_cs_kernel(
 
     // first tile row of instruction i (uniform part) and this lane's row within it
     auto ibase = [&](int i) { return LAYOUT == 0 ? rpi * i : rpi * (i / PER); };
-    // lanes past the instruction's rows, and rows past the workgroup's range, load nothing
-    // (raw-buffer range checks do not cover soffset) and write nothing to the tile
-    auto live = [&](int vb, int i) {
-        const int trow = ibase(i) + prow[i % PER];
-        return i < ni && lactive && trow < 32 && trow < nrows - vb * 32;
-    };
-    // a whole vb in a flat layout: every lane of the first ni instructions is live (uniform test)
-    auto whole = [&](int vb) { return LAYOUT != 0 && nrows - vb * 32 >= 32; };
+    // One code path for every vb (no branches around the loads: divergent paths would make the
+    // compiler join the prefetch registers with moves that wait for the loads right away).
     auto load = [&](int vb, float4* dst) {
-        auto one = [&](int i) __attribute__((always_inline)) {
-            const int soff = (vb * 32 + ibase(i)) * d * 4;
-            const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(xr_rsrc, voff[i % PER], soff, 0);
-            dst[i] = make_float4(__uint_as_float(v[0]), __uint_as_float(v[1]), __uint_as_float(v[2]),
-                                 __uint_as_float(v[3]));
-        };
-        if (whole(vb)) {
 #pragma unroll
-            for (int i = 0; i < NIMAX; ++i)
-                if (i < ni) one(i);
-        } else {
-#pragma unroll
-            for (int i = 0; i < NIMAX; ++i)
-                if (live(vb, i)) one(i);
+        for (int i = 0; i < NIMAX; ++i) {
+            if (i < ni) {  // uniform
+                const uint32_t vo = (uint32_t)voff[i % PER] + (uint32_t)((vb * 32 + ibase(i)) * XS * 4);
+                const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(xr_rsrc, (int)vo, 0, 0);
+                dst[i] = make_float4(__uint_as_float(v[0]), __uint_as_float(v[1]), __uint_as_float(v[2]),
+                                     __uint_as_float(v[3]));
+            }
         }
     };
 
-    float4 xr[NIMAX];
-    int vb = w;
-    if (vb < nvb) load(vb, xr);
-    for (; vb < nvb; vb += kWaves) {
-        // sigma * x -> fp16 -> this wave's tile
-        auto put = [&](int i) __attribute__((always_inline)) {
-            const float2v lo = (float2v){xr[i].x, xr[i].y} * sig2;
-            const float2v hi = (float2v){xr[i].z, xr[i].w} * sig2;
-            *reinterpret_cast<uint2*>(stg + ibase(i) * PITCH + toff[i % PER]) = make_uint2(cvt2(lo.x, lo.y), cvt2(hi.x, hi.y));
-        };
-        if (whole(vb)) {
+    // One step encodes block vb from registers xr and refills xr with block vb + kDepth*kWaves
+    // right after staging it, so kDepth blocks per wave are in flight.
+    auto step = [&](const int vb, float4 (&xr)[NIMAX]) __attribute__((always_inline)) {
+        // sigma * x -> fp16 -> this wave's tile (LAYOUT 0: lanes past the block's rows skip)
 #pragma unroll
-            for (int i = 0; i < NIMAX; ++i)
-                if (i < ni) put(i);
-        } else {
-#pragma unroll
-            for (int i = 0; i < NIMAX; ++i)
-                if (live(vb, i)) put(i);
+        for (int i = 0; i < NIMAX; ++i) {
+            if (i < ni && (LAYOUT != 0 || (lactive && ibase(i) + prow[0] < 32))) {
+                const float2v lo = (float2v){xr[i].x, xr[i].y} * sig2;
+                const float2v hi = (float2v){xr[i].z, xr[i].w} * sig2;
+                *reinterpret_cast<uint2*>(stg + ibase(i) * PITCH + toff[i % PER]) =
+                    make_uint2(cvt2(lo.x, lo.y), cvt2(hi.x, hi.y));
+            }
         }
         lds_fence();
         half8 bf[KS];
@@ -277,7 +268,7 @@ __global__ __launch_bounds__(kThreads) void pq_encode_cs_kernel(
             xx = dot2_self(u[0], xx); xx = dot2_self(u[1], xx);
             xx = dot2_self(u[2], xx); xx = dot2_self(u[3], xx);
         }
-        if (vb + kWaves < nvb && !((V & 64) && vb >= kWaves)) load(vb + kWaves, xr);
+        if (vb + kDepth * kWaves < nvb && !((V & 64) && vb >= kWaves)) load(vb + kDepth * kWaves, xr);
         xx += __shfl_xor(xx, 32);
 
         float t1 = -INFINITY, t2 = -INFINITY, t3 = -INFINITY;
@@ -357,6 +348,16 @@ __global__ __launch_bounds__(kThreads) void pq_encode_cs_kernel(
                 list[basep + __popcll(bp & below)] = make_uint2((uint32_t)rowl, (uint32_t)(k1 | (k2 << 8)));
             if (mine && ncand >= 3) list[nrows - 1 - (basef + __popcll(bfull & below))] = make_uint2((uint32_t)rowl, 0u);
         }
+    };
+    float4 xa[NIMAX], xb[NIMAX];
+    int vb = w;
+    if (vb < nvb) load(vb, xa);
+    if (kDepth == 2 && vb + kWaves < nvb) load(vb + kWaves, xb);
+    for (; vb < nvb; vb += kDepth * kWaves) {
+        step(vb, xa);
+        if (kDepth == 1) continue;
+        if (vb + kWaves >= nvb) break;
+        step(vb + kWaves, xb);
     }
     __syncthreads();
     if (tid == 0) counts[blockIdx.x] = make_int2(ctr[0], ctr[1]);

@@ -4,7 +4,7 @@
 // (/root/reference/src/haag_vq/methods/search/flat_quantized_index.py:45-76), which decodes
 // every code and ranks ||q - x_hat||^2; here the same quantity is assembled from per-query
 // lookup tables, sum_m ||q_m - c_{m,code_m}||^2 (canonical order in include/mivq.h):
-//   adc_lut_kernel     one block per (query, subspace), one lane per centroid.
+//   adc_lut_kernel     one block per (subspace, 32 queries), one lane per centroid.
 //   adc_scan_kernel    LUTs of QB queries live in LDS; each wavefront streams 64 code rows
 //                      per step (one row per lane, 16-B loads), sums M table entries per
 //                      (row, query) and keeps, per query, a wave-resident top-k (element e of
@@ -19,32 +19,76 @@ namespace mivq {
 namespace {
 
 constexpr uint32_t kNoId = 0xFFFFFFFFu;
+typedef float v4f __attribute__((ext_vector_type(4)));  // native vector: HIP's float4 struct copies can defeat SROA
+constexpr int kScanWaves = 16;  // waves per scan workgroup (adc and flat)
 
 __device__ __forceinline__ bool pair_less(float da, uint32_t ia, float db, uint32_t ib) {
     return da < db || (da == db && ia < ib);
 }
 
 // L2: lut[q][m][k] = fmaf chain over t of (q_t - c_t)^2;  IP: -(fmaf chain of q_t * c_t)
-__global__ void adc_lut_kernel(const float* __restrict__ q, int64_t nq, int d, int M, int ksub, int dsub,
-                               const float* __restrict__ C, int metric, float* __restrict__ lut) {
-    const int64_t qm = blockIdx.x;
-    const int64_t qi = qm / M;
-    const int m = (int)(qm % M);
-    const float* qs = q + qi * d + (int64_t)m * dsub;
-    for (int k = threadIdx.x; k < ksub; k += blockDim.x) {
-        const float* c = C + ((int64_t)m * ksub + k) * dsub;
-        float acc = 0.0f;
-        if (metric == MIVQ_METRIC_L2) {
-            for (int t = 0; t < dsub; ++t) {
-                const float df = __fsub_rn(qs[t], c[t]);
-                acc = __builtin_fmaf(df, df, acc);
-            }
-        } else {
-            for (int t = 0; t < dsub; ++t) acc = __builtin_fmaf(qs[t], c[t], acc);
-            acc = -acc;
-        }
-        lut[(qi * M + m) * ksub + k] = acc;
+// grid (M, ceil(nq / kLutQ)), block 256: thread = centroid k of subspace m, looping over a
+// block of kLutQ queries whose sub-vectors sit in LDS (broadcast reads).  The centroid row
+// is read 4 floats at a time and every query's chain advances over those 4 dims in order,
+// so each (query, k) chain is the canonical sequential one.  Stores are coalesced along k.
+constexpr int kLutQ = 32;
+
+__global__ __launch_bounds__(256) void adc_lut_kernel(const float* __restrict__ q, int64_t nq, int d, int M, int ksub,
+                                                       int dsub, const float* __restrict__ C, int metric,
+                                                       float* __restrict__ lut) {
+    extern __shared__ __attribute__((aligned(16))) float qs[];  // [kLutQ][dsub]
+    const int m = blockIdx.x;
+    const int64_t q0 = (int64_t)blockIdx.y * kLutQ;
+    const int nqb = (int)min<int64_t>(kLutQ, nq - q0);
+    for (int e = threadIdx.x; e < nqb * dsub; e += blockDim.x) {
+        const int qq = e / dsub, t = e - qq * dsub;
+        qs[e] = q[(q0 + qq) * d + (int64_t)m * dsub + t];
     }
+    __syncthreads();
+    const int k = threadIdx.x;
+    if (k >= ksub) return;
+    const float* c = C + ((int64_t)m * ksub + k) * dsub;
+    float acc[kLutQ];
+#pragma unroll
+    for (int qq = 0; qq < kLutQ; ++qq) acc[qq] = 0.0f;
+    const bool l2 = metric == MIVQ_METRIC_L2;
+    auto step = [&](float c0, float c1, float c2, float c3, int t0, int nt) __attribute__((always_inline)) {
+#pragma unroll
+        for (int qq = 0; qq < kLutQ; ++qq) {
+            const float* qr = qs + qq * dsub + t0;
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                const float cj = j == 0 ? c0 : j == 1 ? c1 : j == 2 ? c2 : c3;
+                if (j < nt) {
+                    if (l2) {
+                        const float df = __fsub_rn(qr[j], cj);
+                        acc[qq] = __builtin_fmaf(df, df, acc[qq]);
+                    } else {
+                        acc[qq] = __builtin_fmaf(qr[j], cj, acc[qq]);
+                    }
+                }
+            }
+        }
+    };
+    if ((dsub & 3) == 0) {
+        // 16-B loads of the centroid row, the next one in flight while this one is used
+        v4f cur = *reinterpret_cast<const v4f*>(c);
+        for (int t0 = 0; t0 < dsub; t0 += 4) {
+            const v4f nxt = (t0 + 4 < dsub) ? *reinterpret_cast<const v4f*>(c + t0 + 4) : cur;
+            step(cur.x, cur.y, cur.z, cur.w, t0, 4);
+            cur = nxt;
+        }
+    } else {
+        for (int t0 = 0; t0 < dsub; t0 += 4) {
+            const int nt = min(4, dsub - t0);
+            const float c0 = c[t0], c1 = nt > 1 ? c[t0 + 1] : 0.0f;
+            const float c2 = nt > 2 ? c[t0 + 2] : 0.0f, c3 = nt > 3 ? c[t0 + 3] : 0.0f;
+            step(c0, c1, c2, c3, t0, nt);
+        }
+    }
+#pragma unroll
+    for (int qq = 0; qq < kLutQ; ++qq)
+        if (qq < nqb) lut[((q0 + qq) * M + m) * ksub + k] = l2 ? acc[qq] : -acc[qq];
 }
 
 // R = registers per lane of the wave-resident sorted list (k <= 64 * R).
@@ -98,37 +142,59 @@ struct WaveTopK {
     }
 };
 
-// grid (nchunks, ceil(nq / QB)), block 256 (4 waves).  Part index = chunk * 4 + wave.
+// dist[qq] += entry qq of an (m, code) group of QB adjacent floats (16-B aligned for QB >= 4)
+template <int QB>
+__device__ __forceinline__ void lut_add(const float* g, float (&dist)[QB]) {
+    if constexpr (QB >= 4) {
+#pragma unroll
+        for (int v = 0; v < QB / 4; ++v) {
+            const float4 t = *reinterpret_cast<const float4*>(g + 4 * v);
+            dist[4 * v + 0] += t.x; dist[4 * v + 1] += t.y; dist[4 * v + 2] += t.z; dist[4 * v + 3] += t.w;
+        }
+    } else if constexpr (QB == 2) {
+        const float2 t = *reinterpret_cast<const float2*>(g);
+        dist[0] += t.x; dist[1] += t.y;
+    } else {
+        dist[0] += g[0];
+    }
+}
+
+// grid (nchunks, ceil(nq / QB)), block kScanWaves waves sharing the QB LUTs in LDS (so the
+// CU keeps 4 waves per SIMD despite the 128 KiB of tables).  Part index = chunk*kScanWaves + wave.
 template <int R, int QB>
-__global__ __launch_bounds__(256) void adc_scan_kernel(
+__global__ __launch_bounds__(kScanWaves * 64) void adc_scan_kernel(
     const float* __restrict__ lut, int64_t nq, const uint8_t* __restrict__ codes, int64_t n, int M,
     int ksub, int k, int64_t id_offset, int64_t chunk_rows, float* __restrict__ part_d,
     uint32_t* __restrict__ part_i) {
-    extern __shared__ __attribute__((aligned(16))) float tab[];  // [QB][M][ksub]
+    // [M][ksub][QB]: the QB queries' entries of one (m, code) are adjacent, so one 16-B LDS
+    // read serves 4 queries (random codes: ~2x fewer bank-conflict cycles per lookup than
+    // QB separate 4-B reads)
+    extern __shared__ __attribute__((aligned(16))) float tab[];
     const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
     const int64_t q0 = (int64_t)blockIdx.y * QB;
     const int nqb = (int)min<int64_t>(QB, nq - q0);
     const int64_t tab_elems = (int64_t)M * ksub;
-    // stage the LUTs (16-B copies)
-    if ((tab_elems & 3) == 0) {
-        const float4* src = reinterpret_cast<const float4*>(lut + q0 * tab_elems);
-        float4* dst = reinterpret_cast<float4*>(tab);
-        const int64_t cnt = (int64_t)nqb * tab_elems / 4;
-        for (int64_t e = tid; e < cnt; e += 256) dst[e] = src[e];
-    } else {
-        const int64_t cnt = (int64_t)nqb * tab_elems;
-        for (int64_t e = tid; e < cnt; e += 256) tab[e] = lut[q0 * tab_elems + e];
+    for (int64_t e = tid; e < tab_elems * QB; e += kScanWaves * 64) {
+        const int64_t mk = e / QB;
+        const int qq = (int)(e - mk * QB);
+        tab[e] = qq < nqb ? lut[(q0 + qq) * tab_elems + mk] : 0.0f;
     }
     __syncthreads();
 
     WaveTopK<R> top[QB];
+    float thr_d[QB];     // element k-1 of each list (wave-uniform)
+    uint32_t thr_i[QB];
 #pragma unroll
-    for (int qq = 0; qq < QB; ++qq) top[qq].init();
+    for (int qq = 0; qq < QB; ++qq) {
+        top[qq].init();
+        thr_d[qq] = INFINITY;
+        thr_i[qq] = kNoId;
+    }
 
     const int64_t rbeg = (int64_t)blockIdx.x * chunk_rows;
     const int64_t rend = min(n, rbeg + chunk_rows);
     const bool words = (M % 4) == 0;
-    for (int64_t base = rbeg + (int64_t)wv * 64; base < rend; base += 256) {
+    for (int64_t base = rbeg + (int64_t)wv * 64; base < rend; base += kScanWaves * 64) {
         const int64_t row = base + lane;
         const bool valid = row < rend;
         float dist[QB];
@@ -142,17 +208,11 @@ __global__ __launch_bounds__(256) void adc_scan_kernel(
 #pragma unroll
                     for (int b = 0; b < 4; ++b) {
                         const uint32_t code = (wrd >> (8 * b)) & 0xFFu;
-                        const float* tcol = tab + (int64_t)(m0 + b) * ksub + code;
-#pragma unroll
-                        for (int qq = 0; qq < QB; ++qq) dist[qq] += tcol[qq * tab_elems];
+                        lut_add<QB>(tab + ((m0 + b) * ksub + code) * QB, dist);
                     }
                 }
             } else {
-                for (int m = 0; m < M; ++m) {
-                    const float* tcol = tab + (int64_t)m * ksub + cr[m];
-#pragma unroll
-                    for (int qq = 0; qq < QB; ++qq) dist[qq] += tcol[qq * tab_elems];
-                }
+                for (int m = 0; m < M; ++m) lut_add<QB>(tab + (m * ksub + cr[m]) * QB, dist);
             }
         }
         const uint32_t gid = (uint32_t)(id_offset + row);
@@ -161,22 +221,20 @@ __global__ __launch_bounds__(256) void adc_scan_kernel(
             if (qq >= nqb) break;
             float dv = dist[qq];
             if (dv != dv) dv = INFINITY;  // NaN ranks with +inf
-            float kd;
-            uint32_t ki;
-            top[qq].kth(k, kd, ki);
-            unsigned long long mask = __ballot(valid && pair_less(dv, gid, kd, ki));
+            // screen against the cached k-th element; it only moves when something is inserted
+            unsigned long long mask = __ballot(valid && pair_less(dv, gid, thr_d[qq], thr_i[qq]));
             while (mask) {
                 const int src = __builtin_ctzll(mask);
                 mask &= mask - 1;
                 const float cd = __shfl(dv, src);
                 const uint32_t ci = __shfl(gid, src);
-                top[qq].kth(k, kd, ki);
-                if (!pair_less(cd, ci, kd, ki)) continue;
+                if (!pair_less(cd, ci, thr_d[qq], thr_i[qq])) continue;
                 top[qq].insert(cd, ci, k, lane);
+                top[qq].kth(k, thr_d[qq], thr_i[qq]);
             }
         }
     }
-    const int64_t part = (int64_t)blockIdx.x * 4 + wv;
+    const int64_t part = (int64_t)blockIdx.x * kScanWaves + wv;
 #pragma unroll
     for (int qq = 0; qq < QB; ++qq) {
         if (qq >= nqb) break;
@@ -194,22 +252,28 @@ __global__ __launch_bounds__(256) void adc_scan_kernel(
 // query vectors live in LDS; lane = database row, distances are sequential fmaf chains over t
 // (16-B loads of the row), ranked with the same wave-resident top-k as adc_scan_kernel.
 template <int R, int QB>
-__global__ __launch_bounds__(256) void flat_scan_kernel(
+__global__ __launch_bounds__(kScanWaves * 64) void flat_scan_kernel(
     const float* __restrict__ q, int64_t nq, const float* __restrict__ x, int64_t n, int d, int metric, int k,
     int64_t id_offset, int64_t chunk_rows, float* __restrict__ part_d, uint32_t* __restrict__ part_i) {
     extern __shared__ __attribute__((aligned(16))) float qv[];  // [QB][d]
     const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
     const int64_t q0 = (int64_t)blockIdx.y * QB;
     const int nqb = (int)min<int64_t>(QB, nq - q0);
-    for (int64_t e = tid; e < (int64_t)nqb * d; e += 256) qv[e] = q[q0 * d + e];
+    for (int64_t e = tid; e < (int64_t)nqb * d; e += kScanWaves * 64) qv[e] = q[q0 * d + e];
     __syncthreads();
     WaveTopK<R> top[QB];
+    float thr_d[QB];
+    uint32_t thr_i[QB];
 #pragma unroll
-    for (int qq = 0; qq < QB; ++qq) top[qq].init();
+    for (int qq = 0; qq < QB; ++qq) {
+        top[qq].init();
+        thr_d[qq] = INFINITY;
+        thr_i[qq] = kNoId;
+    }
     const int64_t rbeg = (int64_t)blockIdx.x * chunk_rows;
     const int64_t rend = min(n, rbeg + chunk_rows);
     const bool vec = (d % 4) == 0;
-    for (int64_t base = rbeg + (int64_t)wv * 64; base < rend; base += 256) {
+    for (int64_t base = rbeg + (int64_t)wv * 64; base < rend; base += kScanWaves * 64) {
         const int64_t row = base + lane;
         const bool valid = row < rend;
         float dist[QB];
@@ -257,22 +321,19 @@ __global__ __launch_bounds__(256) void flat_scan_kernel(
             if (qq >= nqb) break;
             float dv = metric == MIVQ_METRIC_L2 ? dist[qq] : -dist[qq];
             if (dv != dv) dv = INFINITY;
-            float kd;
-            uint32_t ki;
-            top[qq].kth(k, kd, ki);
-            unsigned long long mask = __ballot(valid && pair_less(dv, gid, kd, ki));
+            unsigned long long mask = __ballot(valid && pair_less(dv, gid, thr_d[qq], thr_i[qq]));
             while (mask) {
                 const int src = __builtin_ctzll(mask);
                 mask &= mask - 1;
                 const float cd = __shfl(dv, src);
                 const uint32_t ci = __shfl(gid, src);
-                top[qq].kth(k, kd, ki);
-                if (!pair_less(cd, ci, kd, ki)) continue;
+                if (!pair_less(cd, ci, thr_d[qq], thr_i[qq])) continue;
                 top[qq].insert(cd, ci, k, lane);
+                top[qq].kth(k, thr_d[qq], thr_i[qq]);
             }
         }
     }
-    const int64_t part = (int64_t)blockIdx.x * 4 + wv;
+    const int64_t part = (int64_t)blockIdx.x * kScanWaves + wv;
 #pragma unroll
     for (int qq = 0; qq < QB; ++qq) {
         if (qq >= nqb) break;
@@ -286,45 +347,59 @@ __global__ __launch_bounds__(256) void flat_scan_kernel(
     }
 }
 
-// One thread per query: k-way selection over `parts` sorted lists laid out (parts, nq, k).
-__global__ void topk_merge_kernel(const float* __restrict__ in_d, const uint32_t* __restrict__ in_i,
-                                  int parts, int64_t nq, int k, float* __restrict__ out_d,
-                                  uint32_t* __restrict__ out_i) {
-    const int64_t qi = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (qi >= nq) return;
-    // cursor per part kept implicitly: count how many of each part were consumed in a
-    // small local array when parts is small, else fall back to a rescan.
-    constexpr int kMaxLocal = 64;
-    int cur_local[kMaxLocal];
-    const bool local = parts <= kMaxLocal;
-    if (local)
-        for (int p = 0; p < parts; ++p) cur_local[p] = 0;
-    float last_d = -INFINITY;
-    uint32_t last_i = 0;
-    bool have_last = false;
-    for (int j = 0; j < k; ++j) {
-        float bd = INFINITY;
-        uint32_t bi = kNoId;
-        int bp = -1;
-        for (int p = 0; p < parts; ++p) {
-            const float* ld = in_d + ((int64_t)p * nq + qi) * k;
-            const uint32_t* li = in_i + ((int64_t)p * nq + qi) * k;
-            int c;
-            if (local) {
-                c = cur_local[p];
-            } else {
-                // first element strictly after (last_d, last_i)
-                c = 0;
-                if (have_last)
-                    while (c < k && !pair_less(last_d, last_i, ld[c], li[c])) ++c;
-            }
-            if (c < k && (bp < 0 || pair_less(ld[c], li[c], bd, bi))) { bd = ld[c]; bi = li[c]; bp = p; }
+// One wave per query: the parts*k candidates (lists laid out (parts, nq, k)) stream through
+// a wave-resident top-k, 64 at a time, screened against the cached k-th element.
+template <int R>
+__global__ __launch_bounds__(256) void topk_merge_kernel(const float* __restrict__ in_d, const uint32_t* __restrict__ in_i,
+                                                         int parts, int64_t nq, int k, float* __restrict__ out_d,
+                                                         uint32_t* __restrict__ out_i) {
+    const int lane = threadIdx.x & 63;
+    const int64_t qi = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (qi >= nq) return;  // whole wave
+    WaveTopK<R> top;
+    top.init();
+    float thr_d = INFINITY;
+    uint32_t thr_i = kNoId;
+    const int64_t total = (int64_t)parts * k;
+    for (int64_t e0 = 0; e0 < total; e0 += 64) {
+        const int64_t e = e0 + lane;
+        const bool valid = e < total;
+        float cd = INFINITY;
+        uint32_t ci = kNoId;
+        if (valid) {
+            const int64_t p = e / k, j = e - p * k;
+            cd = in_d[(p * nq + qi) * k + j];
+            ci = in_i[(p * nq + qi) * k + j];
+            if (cd != cd) cd = INFINITY;
         }
-        if (bp >= 0 && local) cur_local[bp]++;
-        out_d[qi * k + j] = bp >= 0 ? bd : INFINITY;
-        out_i[qi * k + j] = bp >= 0 ? bi : kNoId;
-        last_d = bd; last_i = bi; have_last = true;
+        unsigned long long mask = __ballot(valid && pair_less(cd, ci, thr_d, thr_i));
+        while (mask) {
+            const int src = __builtin_ctzll(mask);
+            mask &= mask - 1;
+            const float vd = __shfl(cd, src);
+            const uint32_t vi = __shfl(ci, src);
+            if (!pair_less(vd, vi, thr_d, thr_i)) continue;
+            top.insert(vd, vi, k, lane);
+            top.kth(k, thr_d, thr_i);
+        }
     }
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+        const int e = r * 64 + lane;
+        if (e < k) { out_d[qi * k + e] = top.d[r]; out_i[qi * k + e] = top.id[r]; }
+    }
+}
+
+hipError_t launch_merge(const float* pd, const uint32_t* pi, int parts, int64_t nq, int k, float* od, uint32_t* oi,
+                        hipStream_t st) {
+    const dim3 grid((unsigned)ceil_div(nq, 4)), block(256);
+    switch ((k + 63) / 64) {
+        case 1: hipLaunchKernelGGL(topk_merge_kernel<1>, grid, block, 0, st, pd, pi, parts, nq, k, od, oi); break;
+        case 2: hipLaunchKernelGGL(topk_merge_kernel<2>, grid, block, 0, st, pd, pi, parts, nq, k, od, oi); break;
+        case 3: hipLaunchKernelGGL(topk_merge_kernel<3>, grid, block, 0, st, pd, pi, parts, nq, k, od, oi); break;
+        default: hipLaunchKernelGGL(topk_merge_kernel<4>, grid, block, 0, st, pd, pi, parts, nq, k, od, oi); break;
+    }
+    return hipGetLastError();
 }
 
 int adc_qb(int M, int ksub) {
@@ -337,10 +412,12 @@ int adc_qb(int M, int ksub) {
     return 0;
 }
 
+// Row chunks per query block: about two workgroups per CU in total, at least one wave-step
+// of rows per wave.
 int64_t adc_chunks(int64_t nq, int64_t n, int QB) {
     const int64_t qblocks = ceil_div(nq, QB);
-    int64_t nch = ceil_div(2048, qblocks);
-    nch = std::max<int64_t>(1, std::min<int64_t>(nch, ceil_div(n, 1024)));
+    int64_t nch = ceil_div(512, qblocks);
+    nch = std::max<int64_t>(1, std::min<int64_t>(nch, ceil_div(n, 64 * kScanWaves)));
     return nch;
 }
 
@@ -352,7 +429,7 @@ hipError_t launch_scan(const float* lut, int64_t nq, const uint8_t* codes, int64
     hipError_t e = hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);
     if (e != hipSuccess) return e;
     const int64_t chunk_rows = ceil_div(n, nch);
-    hipLaunchKernelGGL(kern, dim3((unsigned)nch, (unsigned)ceil_div(nq, QB)), dim3(256), smem, st, lut, nq, codes,
+    hipLaunchKernelGGL(kern, dim3((unsigned)nch, (unsigned)ceil_div(nq, QB)), dim3(kScanWaves * 64), smem, st, lut, nq, codes,
                        n, M, ksub, k, id_offset, chunk_rows, pd, pi);
     return hipGetLastError();
 }
@@ -384,7 +461,7 @@ hipError_t launch_flat(const float* q, int64_t nq, const float* x, int64_t n, in
     auto kern = flat_scan_kernel<R, QB>;
     hipError_t e = hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);
     if (e != hipSuccess) return e;
-    hipLaunchKernelGGL(kern, dim3((unsigned)nch, (unsigned)ceil_div(nq, QB)), dim3(256), smem, st, q, nq, x, n, d,
+    hipLaunchKernelGGL(kern, dim3((unsigned)nch, (unsigned)ceil_div(nq, QB)), dim3(kScanWaves * 64), smem, st, q, nq, x, n, d,
                        metric, k, id_offset, ceil_div(n, nch), pd, pi);
     return hipGetLastError();
 }
@@ -409,7 +486,7 @@ extern "C" size_t mivq_flat_search_workspace_bytes(int64_t nq, int64_t n, int32_
     if (nq <= 0 || n <= 0 || d <= 0 || k <= 0) return 0;
     const int QB = flat_qb(d);
     if (QB == 0) return 0;
-    const int64_t parts = adc_chunks(nq, n, QB) * 4;
+    const int64_t parts = adc_chunks(nq, n, QB) * kScanWaves;
     return align_up((size_t)parts * nq * k * sizeof(float), 256) + align_up((size_t)parts * nq * k * 4, 256);
 }
 
@@ -427,16 +504,16 @@ extern "C" int mivq_flat_search(const float* q, int64_t nq, const float* x, int6
     hipStream_t st = as_stream(stream);
     MIVQ_REQUIRE(dists && ids, MIVQ_ERR_INVALID, "flat_search: null pointer");
     if (n == 0) {
-        hipLaunchKernelGGL(topk_merge_kernel, dim3((unsigned)ceil_div(nq, 256)), dim3(256), 0, st,
-                           (const float*)nullptr, (const uint32_t*)nullptr, 0, nq, k, dists, ids);
-        return check_launch("flat_search(empty)");
+        const hipError_t e = launch_merge(nullptr, nullptr, 0, nq, k, dists, ids, st);
+        if (e != hipSuccess) return set_error(MIVQ_ERR_HIP, "flat_search(empty): %s", hipGetErrorString(e));
+        return MIVQ_OK;
     }
     MIVQ_REQUIRE(q && x, MIVQ_ERR_INVALID, "flat_search: null pointer");
     const size_t need = mivq_flat_search_workspace_bytes(nq, n, d, k);
     MIVQ_REQUIRE(workspace && workspace_bytes >= need, MIVQ_ERR_WORKSPACE, "flat_search: workspace %zu < %zu",
                  workspace_bytes, need);
     const int64_t nch = adc_chunks(nq, n, QB);
-    const int parts = (int)(nch * 4);
+    const int parts = (int)(nch * kScanWaves);
     float* pd = static_cast<float*>(workspace);
     uint32_t* pi = reinterpret_cast<uint32_t*>(static_cast<unsigned char*>(workspace) +
                                                align_up((size_t)parts * nq * k * sizeof(float), 256));
@@ -449,9 +526,9 @@ extern "C" int mivq_flat_search(const float* q, int64_t nq, const float* x, int6
         default: e = launch_flat_r<4>(QB, q, nq, x, n, d, metric, k, id_offset, nch, pd, pi, st); break;
     }
     if (e != hipSuccess) return set_error(MIVQ_ERR_HIP, "flat_scan: %s", hipGetErrorString(e));
-    hipLaunchKernelGGL(topk_merge_kernel, dim3((unsigned)ceil_div(nq, 256)), dim3(256), 0, st, pd, pi, parts, nq, k,
-                       dists, ids);
-    return check_launch("topk_merge");
+    e = launch_merge(pd, pi, parts, nq, k, dists, ids, st);
+    if (e != hipSuccess) return set_error(MIVQ_ERR_HIP, "topk_merge: %s", hipGetErrorString(e));
+    return MIVQ_OK;
 }
 
 extern "C" int mivq_adc_lut(const float* q, int64_t nq, int32_t d, int32_t M, int32_t nbits,
@@ -463,8 +540,10 @@ extern "C" int mivq_adc_lut(const float* q, int64_t nq, int32_t d, int32_t M, in
     if (nq == 0) return MIVQ_OK;
     MIVQ_REQUIRE(q && centroids && lut, MIVQ_ERR_INVALID, "adc_lut: null pointer");
     const int ksub = 1 << nbits;
-    hipLaunchKernelGGL(adc_lut_kernel, dim3((unsigned)(nq * M)), dim3(ksub < 64 ? 64 : ksub), 0, as_stream(stream),
-                       q, nq, d, M, ksub, d / M, centroids, metric, lut);
+    const size_t smem = (size_t)kLutQ * (d / M) * sizeof(float);
+    MIVQ_REQUIRE(smem <= 64 * 1024, MIVQ_ERR_UNSUPPORTED, "adc_lut: dsub=%d too large", d / M);
+    hipLaunchKernelGGL(adc_lut_kernel, dim3((unsigned)M, (unsigned)ceil_div(nq, kLutQ)), dim3(256), smem,
+                       as_stream(stream), q, nq, d, M, ksub, d / M, centroids, metric, lut);
     return check_launch("adc_lut");
 }
 
@@ -472,7 +551,7 @@ extern "C" size_t mivq_adc_search_workspace_bytes(int64_t nq, int64_t n, int32_t
     if (nq <= 0 || n <= 0 || M <= 0 || k <= 0 || nbits < 1 || nbits > 8) return 0;
     const int QB = adc_qb(M, 1 << nbits);
     if (QB == 0) return 0;
-    const int64_t parts = adc_chunks(nq, n, QB) * 4;
+    const int64_t parts = adc_chunks(nq, n, QB) * kScanWaves;
     return align_up((size_t)parts * nq * k * sizeof(float), 256) + align_up((size_t)parts * nq * k * 4, 256);
 }
 
@@ -493,16 +572,16 @@ extern "C" int mivq_adc_search(const float* lut, int64_t nq, const uint8_t* code
     if (n == 0) {
         // nothing to rank: every slot is the sentinel
         MIVQ_REQUIRE(dists && ids, MIVQ_ERR_INVALID, "adc_search: null pointer");
-        hipLaunchKernelGGL(topk_merge_kernel, dim3((unsigned)ceil_div(nq, 256)), dim3(256), 0, st,
-                           (const float*)nullptr, (const uint32_t*)nullptr, 0, nq, k, dists, ids);
-        return check_launch("adc_search(empty)");
+        const hipError_t e = launch_merge(nullptr, nullptr, 0, nq, k, dists, ids, st);
+        if (e != hipSuccess) return set_error(MIVQ_ERR_HIP, "adc_search(empty): %s", hipGetErrorString(e));
+        return MIVQ_OK;
     }
     MIVQ_REQUIRE(lut && codes && dists && ids, MIVQ_ERR_INVALID, "adc_search: null pointer");
     const size_t need = mivq_adc_search_workspace_bytes(nq, n, M, nbits, k);
     MIVQ_REQUIRE(workspace && workspace_bytes >= need, MIVQ_ERR_WORKSPACE, "adc_search: workspace %zu < %zu",
                  workspace_bytes, need);
     const int64_t nch = adc_chunks(nq, n, QB);
-    const int parts = (int)(nch * 4);
+    const int parts = (int)(nch * kScanWaves);
     float* pd = static_cast<float*>(workspace);
     uint32_t* pi = reinterpret_cast<uint32_t*>(static_cast<unsigned char*>(workspace) +
                                                align_up((size_t)parts * nq * k * sizeof(float), 256));
@@ -515,9 +594,9 @@ extern "C" int mivq_adc_search(const float* lut, int64_t nq, const uint8_t* code
         default: e = launch_scan_r<4>(QB, lut, nq, codes, n, M, ksub, k, id_offset, nch, pd, pi, st); break;
     }
     if (e != hipSuccess) return set_error(MIVQ_ERR_HIP, "adc_scan: %s", hipGetErrorString(e));
-    hipLaunchKernelGGL(topk_merge_kernel, dim3((unsigned)ceil_div(nq, 256)), dim3(256), 0, st, pd, pi, parts, nq, k,
-                       dists, ids);
-    return check_launch("topk_merge");
+    e = launch_merge(pd, pi, parts, nq, k, dists, ids, st);
+    if (e != hipSuccess) return set_error(MIVQ_ERR_HIP, "topk_merge: %s", hipGetErrorString(e));
+    return MIVQ_OK;
 }
 
 extern "C" int mivq_topk_merge(const float* dists_in, const uint32_t* ids_in, int32_t parts, int64_t nq, int32_t k,
@@ -526,7 +605,8 @@ extern "C" int mivq_topk_merge(const float* dists_in, const uint32_t* ids_in, in
     if (nq == 0) return MIVQ_OK;
     MIVQ_REQUIRE((parts == 0 || (dists_in && ids_in)) && dists_out && ids_out, MIVQ_ERR_INVALID,
                  "topk_merge: null pointer");
-    hipLaunchKernelGGL(topk_merge_kernel, dim3((unsigned)ceil_div(nq, 256)), dim3(256), 0, as_stream(stream),
-                       dists_in, ids_in, parts, nq, k, dists_out, ids_out);
-    return check_launch("topk_merge");
+    MIVQ_REQUIRE(k <= 256, MIVQ_ERR_UNSUPPORTED, "topk_merge: k=%d > 256", k);
+    const hipError_t e = launch_merge(dists_in, ids_in, parts, nq, k, dists_out, ids_out, as_stream(stream));
+    if (e != hipSuccess) return set_error(MIVQ_ERR_HIP, "topk_merge: %s", hipGetErrorString(e));
+    return MIVQ_OK;
 }

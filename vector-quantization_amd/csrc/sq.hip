@@ -8,7 +8,8 @@
 // astype(uint8/uint16) follows numpy on x86-64: (uintN)(int32)r, every r int32 cannot hold
 // (NaN, +-inf, |r| >= 2^31) -> 0.
 //
-// Layout: one lane handles 8 consecutive dims of a row (HBM-bound, 16-B loads when aligned).
+// Layout: one lane handles 8 consecutive dims of a row (HBM-bound; vector loads and packed
+// stores on the aligned f32 fast path).
 #include "mivq_common.h"
 
 namespace mivq {
@@ -64,6 +65,44 @@ __global__ void sq_encode_kernel(const T* __restrict__ x, int64_t n, int d, cons
     }
 }
 
+// Fast path (f32, d % 8 == 0, 16-B aligned rows): one lane per 8 dims, two 16-B loads of x,
+// lo and den, one 4 / 8 / 16-B store of the packed codes.  Same arithmetic as above.
+__global__ void sq_encode_f32_vec_kernel(const float* __restrict__ x, int64_t n, int d, const float* __restrict__ lo,
+                                         const float* __restrict__ den, int nbits, void* __restrict__ codes) {
+    const uint32_t groups = (uint32_t)(d >> 3);
+    const uint64_t gid = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (gid >= (uint64_t)n * groups) return;
+    const uint64_t i = gid / groups;
+    const int j0 = (int)(gid - i * groups) * 8;
+    const float4* xr = reinterpret_cast<const float4*>(x + i * (uint64_t)d + j0);
+    const float4* lr = reinterpret_cast<const float4*>(lo + j0);
+    const float4* dr = reinterpret_cast<const float4*>(den + j0);
+    const float4 xa = xr[0], xb = xr[1], la = lr[0], lb = lr[1], da = dr[0], db = dr[1];
+    const float L = (float)((1 << nbits) - 1);
+    const float xv[8] = {xa.x, xa.y, xa.z, xa.w, xb.x, xb.y, xb.z, xb.w};
+    const float lv[8] = {la.x, la.y, la.z, la.w, lb.x, lb.y, lb.z, lb.w};
+    const float dv[8] = {da.x, da.y, da.z, da.w, db.x, db.y, db.z, db.w};
+    uint32_t q[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) q[u] = np_cast_uint(sq_step(xv[u], lv[u], dv[u], L));
+    if (nbits == 8) {
+        uint2 w;
+        w.x = (q[0] & 0xFF) | (q[1] & 0xFF) << 8 | (q[2] & 0xFF) << 16 | (q[3] & 0xFF) << 24;
+        w.y = (q[4] & 0xFF) | (q[5] & 0xFF) << 8 | (q[6] & 0xFF) << 16 | (q[7] & 0xFF) << 24;
+        *reinterpret_cast<uint2*>(static_cast<uint8_t*>(codes) + i * (uint64_t)d + j0) = w;
+    } else if (nbits == 16) {
+        uint4 w;
+        w.x = (q[0] & 0xFFFF) | q[1] << 16; w.y = (q[2] & 0xFFFF) | q[3] << 16;
+        w.z = (q[4] & 0xFFFF) | q[5] << 16; w.w = (q[6] & 0xFFFF) | q[7] << 16;
+        *reinterpret_cast<uint4*>(static_cast<uint16_t*>(codes) + i * (uint64_t)d + j0) = w;
+    } else {  // (q[:,0::2] << 4) | q[:,1::2] in uint8 arithmetic
+        uint32_t w = 0;
+#pragma unroll
+        for (int u = 0; u < 8; u += 2) w |= (uint32_t)(uint8_t)(((uint8_t)q[u] << 4) | (uint8_t)q[u + 1]) << (4 * u);
+        *reinterpret_cast<uint32_t*>(static_cast<uint8_t*>(codes) + i * (uint64_t)(d >> 1) + (j0 >> 1)) = w;
+    }
+}
+
 __device__ __forceinline__ float sq_level(const void* codes, int64_t i, int j, int d, int nbits) {
     if (nbits == 16) return (float)static_cast<const uint16_t*>(codes)[i * d + j];
     if (nbits == 8) return (float)static_cast<const uint8_t*>(codes)[i * d + j];
@@ -87,6 +126,43 @@ __global__ void sq_decode_kernel(const void* __restrict__ codes, int64_t n, int 
     }
 }
 
+// Fast decode path (f32 out, d % 8 == 0, aligned): one lane per 8 dims, packed code load, two
+// 16-B stores.
+__global__ void sq_decode_f32_vec_kernel(const void* __restrict__ codes, int64_t n, int d, const float* __restrict__ lo,
+                                         const float* __restrict__ den, int nbits, float* __restrict__ out) {
+    const uint32_t groups = (uint32_t)(d >> 3);
+    const uint64_t gid = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (gid >= (uint64_t)n * groups) return;
+    const uint64_t i = gid / groups;
+    const int j0 = (int)(gid - i * groups) * 8;
+    uint32_t lv[8];
+    if (nbits == 8) {
+        const uint2 w = *reinterpret_cast<const uint2*>(static_cast<const uint8_t*>(codes) + i * (uint64_t)d + j0);
+#pragma unroll
+        for (int u = 0; u < 4; ++u) { lv[u] = (w.x >> (8 * u)) & 0xFF; lv[4 + u] = (w.y >> (8 * u)) & 0xFF; }
+    } else if (nbits == 16) {
+        const uint4 w = *reinterpret_cast<const uint4*>(static_cast<const uint16_t*>(codes) + i * (uint64_t)d + j0);
+        lv[0] = w.x & 0xFFFF; lv[1] = w.x >> 16; lv[2] = w.y & 0xFFFF; lv[3] = w.y >> 16;
+        lv[4] = w.z & 0xFFFF; lv[5] = w.z >> 16; lv[6] = w.w & 0xFFFF; lv[7] = w.w >> 16;
+    } else {  // high nibble = even dim
+        const uint32_t w = *reinterpret_cast<const uint32_t*>(static_cast<const uint8_t*>(codes) + i * (uint64_t)(d >> 1) + (j0 >> 1));
+#pragma unroll
+        for (int u = 0; u < 4; ++u) { const uint32_t b = (w >> (8 * u)) & 0xFF; lv[2 * u] = b >> 4; lv[2 * u + 1] = b & 0xF; }
+    }
+    const float L = (float)((1 << nbits) - 1);
+    const float4* lr = reinterpret_cast<const float4*>(lo + j0);
+    const float4* dr = reinterpret_cast<const float4*>(den + j0);
+    const float4 la = lr[0], lb = lr[1], da = dr[0], db = dr[1];
+    const float lov[8] = {la.x, la.y, la.z, la.w, lb.x, lb.y, lb.z, lb.w};
+    const float dnv[8] = {da.x, da.y, da.z, da.w, db.x, db.y, db.z, db.w};
+    float o[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) o[u] = __fadd_rn(__fmul_rn(__fdiv_rn((float)lv[u], L), dnv[u]), lov[u]);
+    float4* orow = reinterpret_cast<float4*>(out + i * (uint64_t)d + j0);
+    orow[0] = make_float4(o[0], o[1], o[2], o[3]);
+    orow[1] = make_float4(o[4], o[5], o[6], o[7]);
+}
+
 template <typename T>
 int sq_encode(const T* x, int64_t n, int32_t d, const T* lo, const T* den, int32_t nbits, void* codes,
               void* stream, const char* name) {
@@ -96,6 +172,16 @@ int sq_encode(const T* x, int64_t n, int32_t d, const T* lo, const T* den, int32
     if (n == 0) return MIVQ_OK;
     MIVQ_REQUIRE(x && lo && den && codes, MIVQ_ERR_INVALID, "%s: null pointer", name);
     const int64_t work = n * ((d + 7) / 8);
+    if constexpr (sizeof(T) == 4) {
+        const bool vec = (d % 8 == 0) && ((reinterpret_cast<uintptr_t>(x) | reinterpret_cast<uintptr_t>(lo) |
+                                           reinterpret_cast<uintptr_t>(den)) % 16 == 0) &&
+                         (reinterpret_cast<uintptr_t>(codes) % 16 == 0);
+        if (vec) {
+            hipLaunchKernelGGL(sq_encode_f32_vec_kernel, dim3((unsigned)ceil_div(work, 256)), dim3(256), 0,
+                               as_stream(stream), x, n, d, lo, den, nbits, codes);
+            return check_launch(name);
+        }
+    }
     hipLaunchKernelGGL(sq_encode_kernel<T>, dim3((unsigned)ceil_div(work, 256)), dim3(256), 0, as_stream(stream),
                        x, n, d, lo, den, nbits, codes);
     return check_launch(name);
@@ -109,6 +195,15 @@ int sq_decode(const void* codes, int64_t n, int32_t d, const T* lo, const T* den
                  "num_bits must be 4, 8, or 16, got %d", nbits);
     if (n == 0) return MIVQ_OK;
     MIVQ_REQUIRE(codes && lo && den && out, MIVQ_ERR_INVALID, "%s: null pointer", name);
+    if constexpr (sizeof(T) == 4) {
+        const bool vec = (d % 8 == 0) && ((reinterpret_cast<uintptr_t>(codes) | reinterpret_cast<uintptr_t>(lo) |
+                                           reinterpret_cast<uintptr_t>(den) | reinterpret_cast<uintptr_t>(out)) % 16 == 0);
+        if (vec) {
+            hipLaunchKernelGGL(sq_decode_f32_vec_kernel, dim3((unsigned)ceil_div(n * (int64_t)(d / 8), 256)), dim3(256),
+                               0, as_stream(stream), codes, n, d, lo, den, nbits, out);
+            return check_launch(name);
+        }
+    }
     hipLaunchKernelGGL(sq_decode_kernel<T>, dim3((unsigned)ceil_div(n * (int64_t)d, 256)), dim3(256), 0,
                        as_stream(stream), codes, n, d, lo, den, nbits, out);
     return check_launch(name);

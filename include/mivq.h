@@ -179,6 +179,60 @@ int mivq_flat_search(const float* q, int64_t nq, const float* x, int64_t n, int3
 int mivq_topk_merge(const float* dists_in, const uint32_t* ids_in, int32_t parts, int64_t nq,
                     int32_t k, float* dists_out, uint32_t* ids_out, void* stream);
 
+/* ------------------------------------------------------ IVF: coarse quantizer, lists, IVF-PQ
+ * GPU counterpart of FaissIvfPqIndex (methods/search/faiss_ivfpq_index.py:46-76: faiss
+ * IndexIVFPQ over an IndexFlatL2 / IndexFlatIP coarse quantizer, residual PQ) and of the
+ * IVF build in benchmarks/ivf_benchmark.py:170-204.
+ *
+ * Exact pairwise distances, out (n, m) row-major (the coarse quantizer's exhaustive search
+ * and the k-means assignment); the chains of mivq_flat_search:
+ *   L2: out[i][j] = fmaf chain over t ascending of (x_i[t] - y_j[t])^2
+ *   IP: out[i][j] = -(fmaf chain of x_i[t] * y_j[t]) */
+int mivq_pairwise_distances(const float* x, int64_t n, const float* y, int64_t m, int32_t d,
+                            int32_t metric, float* out, void* stream);
+/* Per row of an (n, m) matrix, the k smallest (value, column) pairs ascending (NaN ranks as
+ * +inf, ties to the smaller column); missing slots (m < k) hold (+inf, 0xFFFFFFFF). */
+int mivq_topk_rows(const float* dist, int64_t n, int64_t m, int32_t k, float* out_d,
+                   uint32_t* out_i, void* stream);
+/* Stable bucket sort of assignments (n,) in [0, K), K <= 16384: offsets (K + 1) int64, the
+ * rows of bucket l are order[offsets[l] .. offsets[l+1]) in ascending row order. */
+size_t mivq_bucket_sort_workspace_bytes(int64_t n, int32_t K);
+int mivq_bucket_sort(const uint32_t* assign, int64_t n, int32_t K, int64_t* offsets,
+                     uint32_t* order, void* workspace, size_t workspace_bytes, void* stream);
+/* k-means update from a bucket sort: centroids[l][t] = (f32 sum over the bucket's rows in
+ * ascending row order of x[row][t]) / count for non-empty buckets (empty buckets keep their
+ * value); counts (K,) int32. */
+int mivq_centroid_update(const float* x, int64_t n, int32_t d, int32_t K, const int64_t* offsets,
+                         const uint32_t* order, float* centroids, int32_t* counts, void* stream);
+/* r[i][t] = x[i][t] - coarse[assign[i]][t] */
+int mivq_ivf_residuals(const float* x, int64_t n, int32_t d, const float* coarse,
+                       const uint32_t* assign, float* r, void* stream);
+/* dst row i = src row order[i]; row_bytes a multiple of 4 */
+int mivq_gather_rows(const void* src, int64_t row_bytes, const uint32_t* order, int64_t n,
+                     void* dst, void* stream);
+/* IVF-PQ L2 term per vector (faiss' precomputed table folded per code):
+ *   tau_i = ((t_0 + t_1) + ...) + t_{M-1},  t_m = cn[m][k] + 2 * (fmaf chain over t of
+ *   coarse[assign_i][m*dsub + t] * C[m][k][t]),  k = codes[i][m]
+ * cn = the canonical ||C[m][k]||^2 of mivq_pq_prepare (first block of the prep buffer). */
+int mivq_ivfpq_terms(const uint8_t* codes, int64_t n, int32_t d, int32_t M, int32_t nbits,
+                     const float* pq_centroids, const float* cn, const float* coarse,
+                     const uint32_t* assign, float* tau, void* stream);
+/* IVF-PQ search over inverted lists in bucket order:
+ *   lut (nq, M, ksub): mivq_adc_lut with MIVQ_METRIC_INNER_PRODUCT (= -(q . c) chains)
+ *   probe_d, probe_l (nq, nprobe): coarse distances and list ids (mivq_topk_rows); list id
+ *     0xFFFFFFFF slots are skipped
+ *   offsets (nlist + 1), list_codes (N, M) u8, list_ids (N,), tau (N,) in bucket order
+ *   S = ((lut[q][0][c_0] + lut[q][1][c_1]) + ...) + lut[q][M-1][c_{M-1}]
+ *   L2: dist = (probe_d + tau) + 2 * S  (= ||q - coarse_l - r_hat||^2 expanded)
+ *   IP: dist = probe_d + S              (= -(q . coarse_l + q . r_hat))
+ * ranked like mivq_adc_search: ascending (dist, id) with id = the list_ids entry. */
+size_t mivq_ivfpq_search_workspace_bytes(int64_t nq, int32_t nprobe, int32_t k);
+int mivq_ivfpq_search(const float* lut, int64_t nq, int32_t M, int32_t nbits, const float* probe_d,
+                      const uint32_t* probe_l, int32_t nprobe, int32_t nlist, const int64_t* offsets,
+                      const uint8_t* list_codes, const uint32_t* list_ids, const float* tau,
+                      int32_t metric, int32_t k, void* workspace, size_t workspace_bytes,
+                      float* dists, uint32_t* ids, void* stream);
+
 #pragma GCC visibility pop
 #ifdef __cplusplus
 }

@@ -307,6 +307,102 @@ def extrabitq_decode(codes, c, P, levels, num_bits) -> np.ndarray:
     return ((((sh / np.sqrt(D)) * t[:, None]) @ P.T) * nrm[:, None] + c).astype(np.float32)
 
 
+# ----------------------------------------------------------------------------- IVF / IVF-PQ
+# Restates FaissIvfPqIndex (methods/search/faiss_ivfpq_index.py:46-76; faiss IndexIVFPQ,
+# by_residual) with the canonical arithmetic of include/mivq.h.  PARITY UNPINNED (faiss absent).
+def pairwise(X: np.ndarray, Y: np.ndarray, metric: int = 1) -> np.ndarray:
+    X = np.ascontiguousarray(X, dtype=np.float32)
+    Y = np.ascontiguousarray(Y, dtype=np.float32)
+    out = np.empty((X.shape[0], Y.shape[0]), np.float32)
+    lib().oracle_pairwise(_p(X), _i64(X.shape[0]), _p(Y), _i64(Y.shape[0]), _i32(X.shape[1]), _i32(metric), _p(out))
+    return out
+
+
+def topk_rows(D: np.ndarray, k: int):
+    """Per row the k smallest (value, column) pairs; NaN ranks as +inf; pads (+inf, NO_ID)."""
+    D = np.asarray(D, np.float32)
+    n, m = D.shape
+    key = np.where(np.isnan(D), np.inf, D)
+    order = np.lexsort((np.broadcast_to(np.arange(m), (n, m)), key), axis=1)[:, :k]
+    dd = np.full((n, k), np.inf, np.float32)
+    ii = np.full((n, k), 0xFFFFFFFF, np.uint32)
+    kk = order.shape[1]
+    dd[:, :kk] = np.take_along_axis(key, order, 1)
+    ii[:, :kk] = order.astype(np.uint32)
+    return dd, ii
+
+
+def bucket_sort(assign: np.ndarray, K: int):
+    """(offsets (K+1) int64, order) — rows of each bucket in ascending row order."""
+    assign = np.asarray(assign, np.int64)
+    order = np.argsort(assign, kind="stable").astype(np.uint32)
+    offsets = np.zeros(K + 1, np.int64)
+    offsets[1:] = np.cumsum(np.bincount(assign, minlength=K))
+    return offsets, order
+
+
+def centroid_update(X: np.ndarray, assign: np.ndarray, C: np.ndarray):
+    X = np.ascontiguousarray(X, dtype=np.float32)
+    C = np.array(C, dtype=np.float32, copy=True)
+    K, d = C.shape
+    a = np.ascontiguousarray(assign, dtype=np.uint32)
+    counts = np.empty(K, np.int32)
+    lib().oracle_centroid_update(_p(X), _i64(X.shape[0]), _i32(d), _i32(K), _p(a), _p(C), _p(counts))
+    return C, counts
+
+
+def ivfpq_terms(codes_u8: np.ndarray, Cpq: np.ndarray, coarse: np.ndarray, assign: np.ndarray) -> np.ndarray:
+    codes_u8 = np.ascontiguousarray(codes_u8, dtype=np.uint8)
+    Cpq = np.ascontiguousarray(Cpq, dtype=np.float32)
+    coarse = np.ascontiguousarray(coarse, dtype=np.float32)
+    a = np.ascontiguousarray(assign, dtype=np.uint32)
+    M, ksub, dsub = Cpq.shape
+    cn = pq_norms(Cpq)
+    n = codes_u8.shape[0]
+    tau = np.empty(n, np.float32)
+    lib().oracle_ivfpq_terms(_p(codes_u8), _i64(n), _i32(M * dsub), _i32(M), _i32(ksub), _p(Cpq), _p(cn),
+                             _p(coarse), _p(a), _p(tau))
+    return tau
+
+
+def ivfpq_search(lut, probe_d, probe_l, offsets, list_codes, list_ids, tau, metric: int, k: int):
+    lut = np.ascontiguousarray(lut, dtype=np.float32)
+    nq, M, ksub = lut.shape
+    probe_d = np.ascontiguousarray(probe_d, dtype=np.float32)
+    probe_l = np.ascontiguousarray(probe_l, dtype=np.uint32)
+    offsets = np.ascontiguousarray(offsets, dtype=np.int64)
+    list_codes = np.ascontiguousarray(list_codes, dtype=np.uint8)
+    list_ids = np.ascontiguousarray(list_ids, dtype=np.uint32)
+    tau = np.ascontiguousarray(tau if tau is not None else np.zeros(list_ids.shape[0]), dtype=np.float32)
+    dists = np.empty((nq, k), np.float32)
+    ids = np.empty((nq, k), np.uint32)
+    lib().oracle_ivfpq_search(_p(lut), _i64(nq), _i32(M), _i32(ksub), _p(probe_d), _p(probe_l),
+                              _i32(probe_l.shape[1]), _p(offsets), _p(list_codes), _p(list_ids), _p(tau),
+                              _i32(metric), _i32(k), _p(dists), _p(ids))
+    return dists, ids
+
+
+def ivfpq_build(X: np.ndarray, coarse: np.ndarray, Cpq: np.ndarray, metric: int = 1):
+    """Full IVF-PQ add of X: (assign, codes, offsets, list_codes, list_ids, tau-in-list-order)."""
+    X = np.ascontiguousarray(X, dtype=np.float32)
+    coarse = np.ascontiguousarray(coarse, dtype=np.float32)
+    K = coarse.shape[0]
+    _, a = topk_rows(pairwise(X, coarse, metric), 1)
+    a = a[:, 0]
+    R = (X - coarse[a.astype(np.int64)]).astype(np.float32)
+    codes = pq_encode(R, Cpq)
+    tau = ivfpq_terms(codes, Cpq, coarse, a) if metric == 1 else np.zeros(X.shape[0], np.float32)
+    offsets, order = bucket_sort(a, K)
+    return a, codes, offsets, codes[order], order, tau[order]
+
+
+def ivfpq_query(Q: np.ndarray, coarse: np.ndarray, Cpq: np.ndarray, built, nprobe: int, k: int, metric: int = 1):
+    _, _, offsets, list_codes, list_ids, tau = built
+    pd, pl = topk_rows(pairwise(Q, coarse, metric), nprobe)
+    lut = adc_lut(Q, Cpq, 0)
+    return ivfpq_search(lut, pd, pl, offsets, list_codes, list_ids, tau if metric == 1 else None, metric, k)
+
+
 # ----------------------------------------------------------------------------- metrics
 def exact_l2_topk(Q: np.ndarray, X: np.ndarray, k: int) -> np.ndarray:
     """Exact L2 top-k ids (fp64 distances, stable ties by id) — ground-truth helper."""

@@ -128,3 +128,34 @@ def test_adc_oracle_equals_decode_then_exact(oracle):
     ref = ((Q[:, None, :].astype(np.float64) - Xh[None]) ** 2).sum(-1)
     np.testing.assert_allclose(d, np.take_along_axis(ref, i.astype(np.int64), 1), rtol=1e-5)
     assert np.all(np.diff(d, axis=1) >= 0)
+
+
+def test_ivfpq_oracle_equals_decoded_distances(oracle):
+    """The IVF-PQ restatement's expanded distance (coarse + tau + 2 S, include/mivq.h) equals
+    ||q - (c_l + r_hat)||^2 (and -q.(c_l + r_hat) for IP) to fp32 rounding, with nprobe = K
+    reaching every vector exactly once (faiss_ivfpq_index.py:46-76 semantics)."""
+    rng = np.random.default_rng(4)
+    n, d, K, M = 600, 32, 12, 8
+    X = rng.standard_normal((n, d)).astype(np.float32)
+    Q = rng.standard_normal((7, d)).astype(np.float32)
+    coarse = X[:K].copy()
+    Cpq = (0.5 * rng.standard_normal((M, 256, d // M))).astype(np.float32)
+    for metric in (1, 0):
+        built = oracle.ivfpq_build(X, coarse, Cpq, metric)
+        a, codes = built[0], built[1]
+        xh = coarse[a.astype(np.int64)].astype(np.float64) + oracle.pq_decode(codes, Cpq).astype(np.float64)
+        dd, ii = oracle.ivfpq_query(Q, coarse, Cpq, built, K, n, metric)
+        assert sorted(ii[0].tolist()) == list(range(n))
+        for q in range(len(Q)):
+            if metric == 1:
+                ref = ((Q[q].astype(np.float64) - xh[ii[q].astype(np.int64)]) ** 2).sum(1)
+            else:
+                ref = -(xh[ii[q].astype(np.int64)] @ Q[q].astype(np.float64))
+            np.testing.assert_allclose(dd[q], ref, rtol=1e-4, atol=1e-3)
+
+
+def test_bucket_sort_oracle_is_stable(oracle):
+    a = np.array([3, 1, 3, 0, 1, 3], np.int32)
+    off, order = oracle.bucket_sort(a, 5)
+    assert off.tolist() == [0, 1, 3, 3, 6, 6]
+    assert order.tolist() == [3, 1, 4, 0, 2, 5]

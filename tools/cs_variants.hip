@@ -16,3 +16,43 @@ extern "C" __attribute__((visibility("default"))) int cs_variant(int V, const fl
         default: return -1;
     }
 }
+
+// Read-bandwidth calibration: every byte of x read once with 16-B loads, U independent loads
+// per thread in flight, grid-stride over the buffer; AUX the cache policy (2 = nt).
+template <int U, int AUX>
+__global__ __launch_bounds__(1024) void read_probe_kernel(const float4* __restrict__ x, int64_t n4, uint32_t* out) {
+    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc((void*)x, 0, 0x7FFFFFFF, 0x00020000);
+    uint32_t acc = 0;
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    for (int64_t base = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; base < n4; base += stride * U) {
+        uint32_t v[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const int64_t i = base + u * stride;
+            if (i < n4) {
+                const float4 f = x[i];
+                v[u] = __float_as_uint(f.x) ^ __float_as_uint(f.y) ^ __float_as_uint(f.z) ^ __float_as_uint(f.w);
+            } else {
+                v[u] = 0;
+            }
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) acc ^= v[u];
+    }
+    (void)rs;
+    if (acc == 0x12345678u) out[0] = acc;
+}
+
+extern "C" __attribute__((visibility("default"))) int read_probe(int P, const float* x, int64_t nfloats, void* out,
+                                                                 void* st) {
+    const int64_t n4 = nfloats / 4;
+    hipStream_t s = (hipStream_t)st;
+    switch (P) {
+        case 0: read_probe_kernel<4, 0><<<1024, 1024, 0, s>>>((const float4*)x, n4, (uint32_t*)out); break;
+        case 1: read_probe_kernel<8, 0><<<512, 1024, 0, s>>>((const float4*)x, n4, (uint32_t*)out); break;
+        case 2: read_probe_kernel<12, 0><<<256, 768, 0, s>>>((const float4*)x, n4, (uint32_t*)out); break;
+        case 3: read_probe_kernel<2, 0><<<4096, 1024, 0, s>>>((const float4*)x, n4, (uint32_t*)out); break;
+        default: return -1;
+    }
+    return (int)hipGetLastError();
+}

@@ -59,6 +59,7 @@ def main():
     lib = build()
     dev = _native.require_device()
     X = synth(a.n, a.d, 0, dev, kind=a.data)
+    probes(lib, X, a.reps)
     C = train_pq(X[:65536], a.M, 8, niter=25, seed=1234).contiguous()
     prep = _native.pq_prepare(C, 8)
     ref = _native.pq_encode(X, C, prep, 8)
@@ -100,6 +101,24 @@ def main():
         gbs = a.n * (4 * a.d + a.M) / (ms * 1e-3) / 1e9
         print(f"V={v:2d} {name:32s} {ms:7.3f} ms  {gbs:7.0f} GB/s" + (f"  codes match library: {ok}" if v == 0 else ""),
               flush=True)
+
+
+def probes(lib, X, reps):
+    out = torch.zeros(4, dtype=torch.int32, device=X.device)
+    st = torch.cuda.current_stream().cuda_stream
+    P = ctypes.c_void_p
+    names = {0: "1024x1024 thr, 4 loads/thr", 1: "512x1024, 8 loads/thr", 2: "256x768, 12 loads/thr",
+             3: "4096x1024, 2 loads/thr"}
+    for p, name in names.items():
+        run = lambda: lib.read_probe(ctypes.c_int(p), P(X.data_ptr()), ctypes.c_int64(X.numel()), P(out.data_ptr()), P(st))  # noqa: E731
+        run()
+        torch.cuda.synchronize()
+        ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(reps)]
+        for s, e in ev:
+            s.record(); run(); e.record()
+        torch.cuda.synchronize()
+        ms = sorted(s.elapsed_time(e) for s, e in ev)[reps // 2]
+        print(f"read probe {name:28s} {ms:7.3f} ms  {X.numel() * 4 / (ms * 1e-3) / 1e9:7.0f} GB/s", flush=True)
 
 
 if __name__ == "__main__":

@@ -14,17 +14,13 @@
 //   topk_merge_kernel  merges the per-wave partial lists (and, after the RCCL all-gather,
 //                      the per-shard lists) into the final sorted top-k.
 #include "mivq_common.h"
+#include "topk.h"
 
 namespace mivq {
 namespace {
 
-constexpr uint32_t kNoId = 0xFFFFFFFFu;
 typedef float v4f __attribute__((ext_vector_type(4)));  // native vector: HIP's float4 struct copies can defeat SROA
 constexpr int kScanWaves = 16;  // waves per scan workgroup (adc and flat)
-
-__device__ __forceinline__ bool pair_less(float da, uint32_t ia, float db, uint32_t ib) {
-    return da < db || (da == db && ia < ib);
-}
 
 // L2: lut[q][m][k] = fmaf chain over t of (q_t - c_t)^2;  IP: -(fmaf chain of q_t * c_t)
 // grid (M, ceil(nq / kLutQ)), block 256: thread = centroid k of subspace m, looping over a
@@ -90,57 +86,6 @@ __global__ __launch_bounds__(256) void adc_lut_kernel(const float* __restrict__ 
     for (int qq = 0; qq < kLutQ; ++qq)
         if (qq < nqb) lut[((q0 + qq) * M + m) * ksub + k] = l2 ? acc[qq] : -acc[qq];
 }
-
-// R = registers per lane of the wave-resident sorted list (k <= 64 * R).
-template <int R>
-struct WaveTopK {
-    float d[R];
-    uint32_t id[R];
-
-    __device__ void init() {
-#pragma unroll
-        for (int r = 0; r < R; ++r) { d[r] = INFINITY; id[r] = kNoId; }
-    }
-    // element k-1 (the current threshold); wave-uniform
-    __device__ void kth(int k, float& kd, uint32_t& ki) const {
-        const int r = (k - 1) >> 6, ln = (k - 1) & 63;
-        float vd = d[0];
-        uint32_t vi = id[0];
-#pragma unroll
-        for (int q = 1; q < R; ++q) if (q == r) { vd = d[q]; vi = id[q]; }
-        kd = __shfl(vd, ln);
-        ki = __shfl(vi, ln);
-    }
-    // insert (cd, ci) known to be < element k-1; wave-uniform call
-    __device__ void insert(float cd, uint32_t ci, int k, int lane) {
-        int p = 0;
-#pragma unroll
-        for (int r = 0; r < R; ++r) {
-            const int e = r * 64 + lane;
-            p += __popcll(__ballot(e < k && pair_less(d[r], id[r], cd, ci)));
-        }
-        float nd[R];
-        uint32_t ni[R];
-#pragma unroll
-        for (int r = 0; r < R; ++r) {
-            // element e-1: lane-1 of the same register, or lane 63 of register r-1
-            float pd = __shfl_up(d[r], 1);
-            uint32_t pi = __shfl_up(id[r], 1);
-            float td = INFINITY;
-            uint32_t ti = kNoId;
-            if (r > 0) {  // compile-time r: wave-uniform shuffle
-                td = __shfl(d[r > 0 ? r - 1 : 0], 63);
-                ti = __shfl(id[r > 0 ? r - 1 : 0], 63);
-            }
-            if (lane == 0) { pd = td; pi = ti; }
-            const int e = r * 64 + lane;
-            nd[r] = e > p ? pd : (e == p ? cd : d[r]);
-            ni[r] = e > p ? pi : (e == p ? ci : id[r]);
-        }
-#pragma unroll
-        for (int r = 0; r < R; ++r) { d[r] = nd[r]; id[r] = ni[r]; }
-    }
-};
 
 // dist[qq] += entry qq of an (m, code) group of QB adjacent floats (16-B aligned for QB >= 4)
 template <int QB>
@@ -390,18 +335,6 @@ __global__ __launch_bounds__(256) void topk_merge_kernel(const float* __restrict
     }
 }
 
-hipError_t launch_merge(const float* pd, const uint32_t* pi, int parts, int64_t nq, int k, float* od, uint32_t* oi,
-                        hipStream_t st) {
-    const dim3 grid((unsigned)ceil_div(nq, 4)), block(256);
-    switch ((k + 63) / 64) {
-        case 1: hipLaunchKernelGGL(topk_merge_kernel<1>, grid, block, 0, st, pd, pi, parts, nq, k, od, oi); break;
-        case 2: hipLaunchKernelGGL(topk_merge_kernel<2>, grid, block, 0, st, pd, pi, parts, nq, k, od, oi); break;
-        case 3: hipLaunchKernelGGL(topk_merge_kernel<3>, grid, block, 0, st, pd, pi, parts, nq, k, od, oi); break;
-        default: hipLaunchKernelGGL(topk_merge_kernel<4>, grid, block, 0, st, pd, pi, parts, nq, k, od, oi); break;
-    }
-    return hipGetLastError();
-}
-
 int adc_qb(int M, int ksub) {
     const int64_t per = (int64_t)M * ksub * 4;
     const int64_t budget = 128 * 1024;
@@ -478,6 +411,19 @@ hipError_t launch_flat_r(int QB, const float* q, int64_t nq, const float* x, int
 }
 
 }  // namespace
+
+hipError_t launch_topk_merge(const float* pd, const uint32_t* pi, int parts, int64_t nq, int k, float* od, uint32_t* oi,
+                        hipStream_t st) {
+    const dim3 grid((unsigned)ceil_div(nq, 4)), block(256);
+    switch ((k + 63) / 64) {
+        case 1: hipLaunchKernelGGL(topk_merge_kernel<1>, grid, block, 0, st, pd, pi, parts, nq, k, od, oi); break;
+        case 2: hipLaunchKernelGGL(topk_merge_kernel<2>, grid, block, 0, st, pd, pi, parts, nq, k, od, oi); break;
+        case 3: hipLaunchKernelGGL(topk_merge_kernel<3>, grid, block, 0, st, pd, pi, parts, nq, k, od, oi); break;
+        default: hipLaunchKernelGGL(topk_merge_kernel<4>, grid, block, 0, st, pd, pi, parts, nq, k, od, oi); break;
+    }
+    return hipGetLastError();
+}
+
 }  // namespace mivq
 
 using namespace mivq;
@@ -504,7 +450,7 @@ extern "C" int mivq_flat_search(const float* q, int64_t nq, const float* x, int6
     hipStream_t st = as_stream(stream);
     MIVQ_REQUIRE(dists && ids, MIVQ_ERR_INVALID, "flat_search: null pointer");
     if (n == 0) {
-        const hipError_t e = launch_merge(nullptr, nullptr, 0, nq, k, dists, ids, st);
+        const hipError_t e = launch_topk_merge(nullptr, nullptr, 0, nq, k, dists, ids, st);
         if (e != hipSuccess) return set_error(MIVQ_ERR_HIP, "flat_search(empty): %s", hipGetErrorString(e));
         return MIVQ_OK;
     }
@@ -526,7 +472,7 @@ extern "C" int mivq_flat_search(const float* q, int64_t nq, const float* x, int6
         default: e = launch_flat_r<4>(QB, q, nq, x, n, d, metric, k, id_offset, nch, pd, pi, st); break;
     }
     if (e != hipSuccess) return set_error(MIVQ_ERR_HIP, "flat_scan: %s", hipGetErrorString(e));
-    e = launch_merge(pd, pi, parts, nq, k, dists, ids, st);
+    e = launch_topk_merge(pd, pi, parts, nq, k, dists, ids, st);
     if (e != hipSuccess) return set_error(MIVQ_ERR_HIP, "topk_merge: %s", hipGetErrorString(e));
     return MIVQ_OK;
 }
@@ -572,7 +518,7 @@ extern "C" int mivq_adc_search(const float* lut, int64_t nq, const uint8_t* code
     if (n == 0) {
         // nothing to rank: every slot is the sentinel
         MIVQ_REQUIRE(dists && ids, MIVQ_ERR_INVALID, "adc_search: null pointer");
-        const hipError_t e = launch_merge(nullptr, nullptr, 0, nq, k, dists, ids, st);
+        const hipError_t e = launch_topk_merge(nullptr, nullptr, 0, nq, k, dists, ids, st);
         if (e != hipSuccess) return set_error(MIVQ_ERR_HIP, "adc_search(empty): %s", hipGetErrorString(e));
         return MIVQ_OK;
     }
@@ -594,7 +540,7 @@ extern "C" int mivq_adc_search(const float* lut, int64_t nq, const uint8_t* code
         default: e = launch_scan_r<4>(QB, lut, nq, codes, n, M, ksub, k, id_offset, nch, pd, pi, st); break;
     }
     if (e != hipSuccess) return set_error(MIVQ_ERR_HIP, "adc_scan: %s", hipGetErrorString(e));
-    e = launch_merge(pd, pi, parts, nq, k, dists, ids, st);
+    e = launch_topk_merge(pd, pi, parts, nq, k, dists, ids, st);
     if (e != hipSuccess) return set_error(MIVQ_ERR_HIP, "topk_merge: %s", hipGetErrorString(e));
     return MIVQ_OK;
 }
@@ -606,7 +552,7 @@ extern "C" int mivq_topk_merge(const float* dists_in, const uint32_t* ids_in, in
     MIVQ_REQUIRE((parts == 0 || (dists_in && ids_in)) && dists_out && ids_out, MIVQ_ERR_INVALID,
                  "topk_merge: null pointer");
     MIVQ_REQUIRE(k <= 256, MIVQ_ERR_UNSUPPORTED, "topk_merge: k=%d > 256", k);
-    const hipError_t e = launch_merge(dists_in, ids_in, parts, nq, k, dists_out, ids_out, as_stream(stream));
+    const hipError_t e = launch_topk_merge(dists_in, ids_in, parts, nq, k, dists_out, ids_out, as_stream(stream));
     if (e != hipSuccess) return set_error(MIVQ_ERR_HIP, "topk_merge: %s", hipGetErrorString(e));
     return MIVQ_OK;
 }

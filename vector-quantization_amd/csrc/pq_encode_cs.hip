@@ -51,6 +51,7 @@ constexpr int kWaves = 12;  // 768 threads, 3 waves per SIMD
 constexpr int kDepth = 1;   // x blocks in flight per wave
 constexpr int kThreads = kWaves * 64;
 constexpr int kRsrcWord3 = 0x00020000;  // gfx9 buffer resource: 32-bit data format
+constexpr int kXAux = 2;  // x stream cache policy: nt (read once)
 
 // Keeps the three largest of a stream of packed scores.  Inline asm because the compiler
 // quiets every packed value (v_max_f32 v, v, v) before fmaxf / fmed3 in IEEE mode: the
@@ -238,7 +239,7 @@ __global__ __launch_bounds__(kThreads) void pq_encode_cs_kernel(
         for (int i = 0; i < NIMAX; ++i) {
             if (i < ni) {  // uniform
                 const uint32_t vo = (uint32_t)voff[i % PER] + (uint32_t)((vb * 32 + ibase(i)) * XS * 4);
-                const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(xr_rsrc, (int)vo, 0, 0);
+                const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(xr_rsrc, (int)vo, 0, kXAux);
                 dst[i] = make_float4(__uint_as_float(v[0]), __uint_as_float(v[1]), __uint_as_float(v[2]),
                                      __uint_as_float(v[3]));
             }
@@ -470,7 +471,6 @@ __global__ __launch_bounds__(kRWaves * 64) void pq_resolve_cs_kernel(
             if constexpr ((V & 10) != 0) { lds_fence(); continue; }
             constexpr int G = 8;
             const float* ca = cp + l * PP;
-            const float* cb = cp + (l + 64) * PP;
             for (int g0 = 0; g0 < cntb; g0 += G) {
                 float2v a[G], bb[G];
 #pragma unroll

@@ -69,6 +69,17 @@ SIGNATURES = {
     "mivq_flat_search_workspace_bytes": (_sz, [_i64, _i64, _i32, _i32]),
     "mivq_flat_search": (_c.c_int, [_vp, _i64, _vp, _i64, _i32, _i32, _i32, _i64, _vp, _sz, _vp, _vp, _vp]),
     "mivq_topk_merge": (_c.c_int, [_vp, _vp, _i32, _i64, _i32, _vp, _vp, _vp]),
+    "mivq_pairwise_distances": (_c.c_int, [_vp, _i64, _vp, _i64, _i32, _i32, _vp, _vp]),
+    "mivq_topk_rows": (_c.c_int, [_vp, _i64, _i64, _i32, _vp, _vp, _vp]),
+    "mivq_bucket_sort_workspace_bytes": (_sz, [_i64, _i32]),
+    "mivq_bucket_sort": (_c.c_int, [_vp, _i64, _i32, _vp, _vp, _vp, _sz, _vp]),
+    "mivq_centroid_update": (_c.c_int, [_vp, _i64, _i32, _i32, _vp, _vp, _vp, _vp, _vp]),
+    "mivq_ivf_residuals": (_c.c_int, [_vp, _i64, _i32, _vp, _vp, _vp, _vp]),
+    "mivq_gather_rows": (_c.c_int, [_vp, _i64, _vp, _i64, _vp, _vp]),
+    "mivq_ivfpq_terms": (_c.c_int, [_vp, _i64, _i32, _i32, _i32, _vp, _vp, _vp, _vp, _vp, _vp]),
+    "mivq_ivfpq_search_workspace_bytes": (_sz, [_i64, _i32, _i32]),
+    "mivq_ivfpq_search": (_c.c_int, [_vp, _i64, _i32, _i32, _vp, _vp, _i32, _i32, _vp, _vp, _vp, _vp, _i32, _i32,
+                                     _vp, _sz, _vp, _vp, _vp]),
 }
 
 _lib: Optional[ctypes.CDLL] = None
@@ -412,3 +423,123 @@ def topk_merge(dists: torch.Tensor, ids: torch.Tensor, k: int) -> Tuple[torch.Te
     oi = torch.empty((nq, k), dtype=torch.int32, device=dists.device)
     _call("mivq_topk_merge", _ptr(dists), _ptr(ids), parts, nq, k, _ptr(od), _ptr(oi), _stream())
     return od, oi
+
+
+# ----------------------------------------------------------------- IVF
+def pairwise_distances(x: torch.Tensor, y: torch.Tensor, metric: int = METRIC_L2,
+                       out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """(n, m) exact chains: L2 sum (x-y)^2, IP -(x . y)."""
+    _check(x, "x", torch.float32, 2)
+    _check(y, "y", torch.float32, 2)
+    n, d = x.shape
+    m = y.shape[0]
+    if y.shape[1] != d:
+        raise ValueError(f"pairwise_distances: d mismatch {d} vs {y.shape[1]}")
+    if out is None:
+        out = torch.empty((n, m), dtype=torch.float32, device=x.device)
+    else:
+        _check(out, "out", torch.float32, 2)
+        if tuple(out.shape) != (n, m):
+            raise ValueError("pairwise_distances: out has the wrong shape")
+    _call("mivq_pairwise_distances", _ptr(x), n, _ptr(y), m, d, metric, _ptr(out), _stream())
+    return out
+
+
+def topk_rows(dist: torch.Tensor, k: int) -> Tuple[torch.Tensor, torch.Tensor]:
+    """Per row the k smallest (value, column); ids int32 holding uint32 bit patterns."""
+    _check(dist, "dist", torch.float32, 2)
+    n, m = dist.shape
+    od = torch.empty((n, k), dtype=torch.float32, device=dist.device)
+    oi = torch.empty((n, k), dtype=torch.int32, device=dist.device)
+    _call("mivq_topk_rows", _ptr(dist), n, m, k, _ptr(od), _ptr(oi), _stream())
+    return od, oi
+
+
+def bucket_sort(assign: torch.Tensor, K: int) -> Tuple[torch.Tensor, torch.Tensor]:
+    """Stable bucket sort of (n,) int32 assignments: (offsets int64 (K+1), order int32 (n))."""
+    _check(assign, "assign", torch.int32, 1)
+    n = assign.shape[0]
+    offsets = torch.empty(K + 1, dtype=torch.int64, device=assign.device)
+    order = torch.empty(n, dtype=torch.int32, device=assign.device)
+    nb = load_library().mivq_bucket_sort_workspace_bytes(n, K)
+    ws = workspace(nb, assign.device)
+    _call("mivq_bucket_sort", _ptr(assign), n, K, _ptr(offsets), _ptr(order), _ptr(ws), ws.numel(), _stream())
+    return offsets, order
+
+
+def centroid_update(x: torch.Tensor, offsets: torch.Tensor, order: torch.Tensor, centroids: torch.Tensor,
+                    counts: torch.Tensor) -> None:
+    _check(x, "x", torch.float32, 2)
+    _check(offsets, "offsets", torch.int64, 1)
+    _check(order, "order", torch.int32, 1)
+    _check(centroids, "centroids", torch.float32, 2)
+    _check(counts, "counts", torch.int32, 1)
+    n, d = x.shape
+    K = centroids.shape[0]
+    if centroids.shape[1] != d or offsets.shape[0] != K + 1 or counts.shape[0] != K or order.shape[0] != n:
+        raise ValueError("centroid_update: shape mismatch")
+    _call("mivq_centroid_update", _ptr(x), n, d, K, _ptr(offsets), _ptr(order), _ptr(centroids), _ptr(counts),
+          _stream())
+
+
+def ivf_residuals(x: torch.Tensor, coarse: torch.Tensor, assign: torch.Tensor,
+                  out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    _check(x, "x", torch.float32, 2)
+    _check(coarse, "coarse", torch.float32, 2)
+    _check(assign, "assign", torch.int32, 1)
+    n, d = x.shape
+    if coarse.shape[1] != d or assign.shape[0] != n:
+        raise ValueError("ivf_residuals: shape mismatch")
+    r = torch.empty_like(x) if out is None else out
+    _call("mivq_ivf_residuals", _ptr(x), n, d, _ptr(coarse), _ptr(assign), _ptr(r), _stream())
+    return r
+
+
+def gather_rows(src: torch.Tensor, order: torch.Tensor) -> torch.Tensor:
+    """dst[i] = src[order[i]] for a contiguous (n, ...) tensor whose rows are 4-byte multiples."""
+    _check(order, "order", torch.int32, 1)
+    if not src.is_cuda or not src.is_contiguous():
+        raise ValueError("gather_rows: src must be a contiguous device tensor")
+    row_bytes = src[0].numel() * src.element_size() if src.shape[0] else src.element_size()
+    dst = torch.empty((order.shape[0],) + tuple(src.shape[1:]), dtype=src.dtype, device=src.device)
+    _call("mivq_gather_rows", _ptr(src), row_bytes, _ptr(order), order.shape[0], _ptr(dst), _stream())
+    return dst
+
+
+def ivfpq_terms(codes_u8: torch.Tensor, pq_centroids: torch.Tensor, prep: torch.Tensor, coarse: torch.Tensor,
+                assign: torch.Tensor, nbits: int) -> torch.Tensor:
+    _check(codes_u8, "codes", torch.uint8, 2)
+    _check(pq_centroids, "pq_centroids", torch.float32, 3)
+    _check(coarse, "coarse", torch.float32, 2)
+    _check(assign, "assign", torch.int32, 1)
+    n, M = codes_u8.shape
+    d = coarse.shape[1]
+    tau = torch.empty(n, dtype=torch.float32, device=codes_u8.device)
+    _call("mivq_ivfpq_terms", _ptr(codes_u8), n, d, M, nbits, _ptr(pq_centroids), _ptr(prep), _ptr(coarse),
+          _ptr(assign), _ptr(tau), _stream())
+    return tau
+
+
+def ivfpq_search(lut: torch.Tensor, probe_d: torch.Tensor, probe_l: torch.Tensor, offsets: torch.Tensor,
+                 list_codes: torch.Tensor, list_ids: torch.Tensor, tau: Optional[torch.Tensor], metric: int,
+                 k: int, nbits: int) -> Tuple[torch.Tensor, torch.Tensor]:
+    _check(lut, "lut", torch.float32, 3)
+    _check(probe_d, "probe_d", torch.float32, 2)
+    _check(probe_l, "probe_l", torch.int32, 2)
+    _check(offsets, "offsets", torch.int64, 1)
+    _check(list_codes, "list_codes", torch.uint8, 2)
+    _check(list_ids, "list_ids", torch.int32, 1)
+    if tau is not None:
+        _check(tau, "tau", torch.float32, 1)
+    nq, M, _ = lut.shape
+    nprobe = probe_l.shape[1]
+    nlist = offsets.shape[0] - 1
+    dists = torch.empty((nq, k), dtype=torch.float32, device=lut.device)
+    ids = torch.empty((nq, k), dtype=torch.int32, device=lut.device)
+    nb = load_library().mivq_ivfpq_search_workspace_bytes(nq, nprobe, k)
+    ws = workspace(nb, lut.device)
+    _call("mivq_ivfpq_search", _ptr(lut), nq, M, nbits, _ptr(probe_d), _ptr(probe_l), nprobe, nlist, _ptr(offsets),
+          _ptr(list_codes), _ptr(list_ids), _ptr(tau), metric, k, _ptr(ws), ws.numel(), _ptr(dists), _ptr(ids),
+          _stream())
+    return dists, ids
+

@@ -1,12 +1,15 @@
 """Throughput of the other BASELINE.json configs on 1 GPU (bench.py measures the headline PQ16).
 
-usage: python tools/bench_configs.py --workload opq32|sq8|rabitq1 [--n N] [--steps K] [--warmup W]
+usage: python tools/bench_configs.py --workload opq32|sq8|rabitq1|ivfpq [--n N] [--steps K] [--warmup W]
 
   opq32   configs[2]: OPQ M=32 B=8 encode of 1M x 1536 (rotation on fp32 MFMA + PQ32 encode)
           and ADC recall@10 / queries/s (queries rotated, LUT + scan), OPQ trained on 65,536 rows.
   sq8     configs[3]: SQ-8 encode of 1M x 3072 (fit = per-dim min/max), and search by decode +
           exact scan (the reference's SQ search) for 100 queries.
   rabitq1 configs[3]: RaBitQ 1-bit encode of 1M x 3072, search by decode + exact scan.
+  ivfpq   SURVEY §8f rank 2: FaissIvfPqIndex defaults (K 4096, m 16, nbits 8, nprobe 200)
+          over 1M x 1536: build (coarse k-means + residual PQ + add) time, search queries/s
+          and recall@10 against exact ground truth.
 
 Prints one JSON line in bench.py's format (roofline of the dominant kernel, HIP-event timing).
 """
@@ -138,9 +141,51 @@ def run_flatcodes(a, dev, kind):
     }
 
 
+def run_ivfpq(a, dev):
+    from haag_vq.methods._ivf import IvfPq
+
+    d, K, M = 1536, a.nlist, 16
+    X = synth(a.n, d, seed=0, dev=dev, kind="clustered")
+    idx = IvfPq(d, K, M, 8)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    idx.train(X)
+    torch.cuda.synchronize()
+    t_train = time.perf_counter() - t0
+    t0 = time.perf_counter()
+    idx.add(X)
+    torch.cuda.synchronize()
+    t_add = time.perf_counter() - t0
+    Q = synth(a.nq, d, seed=1_000_003, dev=dev, kind="clustered")
+    res = {}
+    for nprobe in (a.nprobe, 16):
+        swall, sdev = timed(lambda: idx.search(Q, 10, nprobe), a.steps, 1)
+        _, ii = idx.search(Q[:100].contiguous(), 10, nprobe)
+        _, gi = _native.flat_search(Q[:100].contiguous(), X, 10)
+        res[nprobe] = {"qps": a.nq / swall, "ms_per_batch": swall * 1e3,
+                       "recall@10": recall(gi.cpu().numpy(), ii.cpu().numpy(), 10)}
+    # coarse-assignment kernel rate: one (rows x K x d) pairwise pass over 65,536 rows
+    xs = X[:65536].contiguous()
+    out = torch.empty((xs.shape[0], K), dtype=torch.float32, device=dev)
+    _, pw_ms = timed(lambda: _native.pairwise_distances(xs, idx.coarse, _native.METRIC_L2, out=out), 5, 1)
+    pair_steps = xs.shape[0] * K * d
+    return {
+        "metric": "IVF-PQ (K 4096, PQ16x8, nprobe 200) search queries/sec @ recall@10, 1M x 1536 fp32",
+        "value": res[a.nprobe]["qps"], "unit": "queries/s", "ms_per_step": res[a.nprobe]["ms_per_batch"],
+        "dtype": "f32", "config": {"workload": f"ivfpq_{a.n}x{d}", "nlist": K, "M": M, "nbits": 8,
+                                    "nprobe": a.nprobe, "nq": a.nq, "k": 10},
+        "search": res, "build_s": {"train": t_train, "add": t_add},
+        "pairwise_kernel": {"ms": pw_ms, "rows": xs.shape[0], "cols": K, "d": d,
+                            "pair_steps_per_s": pair_steps / (pw_ms * 1e-3),
+                            "note": "sequential fmaf chains (sub + fma per pair-step) on packed fp32 VALU"},
+    }
+
+
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--workload", choices=("opq32", "sq8", "rabitq1"), required=True)
+    ap.add_argument("--workload", choices=("opq32", "sq8", "rabitq1", "ivfpq"), required=True)
+    ap.add_argument("--nlist", type=int, default=4096)
+    ap.add_argument("--nprobe", type=int, default=200)
     ap.add_argument("--n", type=int, default=1_000_000)
     ap.add_argument("--nq", type=int, default=1000)
     ap.add_argument("--steps", type=int, default=10)
@@ -148,7 +193,12 @@ def main():
     ap.add_argument("--opq-iters", type=int, default=10)
     a = ap.parse_args()
     dev = _native.require_device()
-    out = run_opq32(a, dev) if a.workload == "opq32" else run_flatcodes(a, dev, a.workload)
+    if a.workload == "opq32":
+        out = run_opq32(a, dev)
+    elif a.workload == "ivfpq":
+        out = run_ivfpq(a, dev)
+    else:
+        out = run_flatcodes(a, dev, a.workload)
     out.update({"n_gpus": 1, "steps": a.steps, "warmup": a.warmup, "higher_is_better": True, "data": "synthetic"})
     print(json.dumps(out), flush=True)
 

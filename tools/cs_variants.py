@@ -22,7 +22,9 @@ from bench import synth  # noqa: E402
 VARIANTS = {0: "encode + resolve", 1: "encode only", 2: "resolve: pairs only", 4: "resolve: full scans only",
             8: "resolve: gathers, no compute", 33: "encode only, 1 of 8 cb",
             17: "loads + convert + tile + fragments only", 65: "encode only, no x loads (compute alone)",
-            145: "streaming only, subspace-major probe"}
+            145: "streaming only, subspace-major probe", 256: "encode + resolve, 256-wide full scans",
+            513: "encode + full-item kernel", 1537: "... no exact chains", 2561: "... 1 of 8 filter blocks",
+            4609: "... no gathers", 7681: "... none of the three"}
 
 
 def prep_layout(M, dsub, ksub=256):
@@ -55,6 +57,7 @@ def main():
     ap.add_argument("--M", type=int, default=16)
     ap.add_argument("--reps", type=int, default=10)
     ap.add_argument("--data", default="clustered")
+    ap.add_argument("--ab", default="", help="V1,V2: interleaved A/B timing instead of the variant table")
     a = ap.parse_args()
     lib = build()
     dev = _native.require_device()
@@ -79,6 +82,34 @@ def main():
                             P(items.data_ptr()), P(counts.data_ptr()), P(st))
         assert rc == 0, rc
 
+    if a.ab:
+        va, vb = (int(t) for t in a.ab.split(","))
+        res = {va: [], vb: []}
+        for v in (va, vb):
+            run(v)
+        torch.cuda.synchronize()
+        for _ in range(a.reps * 3):
+            for v in (va, vb):
+                s_, e_ = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                s_.record(); run(v); e_.record()
+                torch.cuda.synchronize()
+                res[v].append(s_.elapsed_time(e_))
+        for v in (va, vb):
+            t = sorted(res[v])
+            print(f"AB V={v}: median {t[len(t) // 2]:.3f} ms  min {t[0]:.3f}  max {t[-1]:.3f}", flush=True)
+        return
+    # instrumentation: V=513 runs encode + the full-item kernel with counting (no pair
+    # kernel); counts then hold the tallies
+    counts.zero_()
+    run(0)
+    torch.cuda.synchronize()
+    c0 = counts.clone()
+    run(513)
+    torch.cuda.synchronize()
+    diff = (counts - c0).long()
+    rows = int((diff[:, 0] & 0xFFFF).sum()); scans = int((diff[:, 0] >> 16).sum()); cands = int((diff[:, 1] >> 8).sum())
+    print(f"full kernel: rows {rows}, whole-row scans {scans}, candidates {cands} ({cands / max(rows, 1):.2f}/row)",
+          flush=True)
     for v, name in VARIANTS.items():
         run(v)
         torch.cuda.synchronize()

@@ -150,7 +150,10 @@ constexpr int max_loads() {
 // produce wrong codes: 1 the resolve kernel, 2 its full scans, 4 its pair checks, 8 its x
 // reads, 16 the whole filter, 32 all but the first 32 centroids of the filter, 64 the x
 // loads after a wave's second vb (compute alone), 128 reads the same bytes as if x were
-// stored subspace-major (contiguous per workgroup: a memory-pattern probe).
+// stored subspace-major (contiguous per workgroup: a memory-pattern probe), 256 settles full
+// items with the pair kernel's 256-wide exact scans instead of pq_resolve_full_kernel, 512
+// makes that kernel count (into `counts`) its rows, whole-row scans and candidates; with 512:
+// 1024 skips its exact chains, 2048 runs one filter block, 4096 gathers row 0 only.
 template <int KS, int LAYOUT, int V = 0>
 __global__ __launch_bounds__(kThreads) void pq_encode_cs_kernel(
     const float* __restrict__ x, int64_t n, int d, int M, int dsub, int64_t rows_per_wg,
@@ -383,7 +386,7 @@ template <int KS, int V = 0>
 __global__ __launch_bounds__(kRWaves * 64) void pq_resolve_cs_kernel(
     const float* __restrict__ x, int64_t n, int d, int M, int dsub, int64_t rows_per_wg,
     const float* __restrict__ C, const float* __restrict__ cn, uint8_t* __restrict__ codesT,
-    const uint2* __restrict__ items, const int2* __restrict__ counts) {
+    const uint2* __restrict__ items, const int2* __restrict__ counts, int with_full) {
     constexpr int DP = 16 * KS;
     constexpr int PP = 2 * DP + 4;  // floats per centroid-pair row
     constexpr int SP = DP + 4;      // floats per staged x row
@@ -404,16 +407,33 @@ __global__ __launch_bounds__(kRWaves * 64) void pq_resolve_cs_kernel(
     if (r0 >= r1) return;
     const int nrows = (int)(r1 - r0);
     const int2 cnt = counts[blockIdx.x];
-    const int np = cnt.x, nf = cnt.y;
+    const int np = cnt.x, nf = with_full ? cnt.y : 0;
     if (np + nf == 0) return;
 
-    {
+    {  // pairs (kp, kp + 128) interleaved; 16-B loads, 4 chunk pairs in flight per thread
         const float* Cm = C + (int64_t)m * 256 * dsub;
-        for (int e = tid; e < 128 * DP; e += kRWaves * 64) {
-            const int kp = e / DP, t = e - kp * DP;
-            const bool in = t < dsub;
-            *reinterpret_cast<float2*>(cp + kp * PP + 2 * t) =
-                make_float2(in ? Cm[(int64_t)kp * dsub + t] : 0.0f, in ? Cm[(int64_t)(kp + 128) * dsub + t] : 0.0f);
+        const int q4 = DP >> 2, tot = 128 * q4;
+        for (int e0 = tid; e0 < tot; e0 += 4 * kRWaves * 64) {
+            f32x4 va[4], vb[4];
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                const int e = e0 + u * kRWaves * 64;
+                const int kp = e / q4, j = e - kp * q4;
+                const bool in = e < tot && 4 * j < dsub;
+                va[u] = in ? *reinterpret_cast<const f32x4*>(Cm + (int64_t)kp * dsub + 4 * j) : (f32x4){0.f, 0.f, 0.f, 0.f};
+                vb[u] = in ? *reinterpret_cast<const f32x4*>(Cm + (int64_t)(kp + 128) * dsub + 4 * j)
+                           : (f32x4){0.f, 0.f, 0.f, 0.f};
+            }
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                const int e = e0 + u * kRWaves * 64;
+                const int kp = e / q4, j = e - kp * q4;
+                if (e < tot) {
+                    f32x4* dst = reinterpret_cast<f32x4*>(cp + kp * PP + 8 * j);
+                    dst[0] = (f32x4){va[u].x, vb[u].x, va[u].y, vb[u].y};
+                    dst[1] = (f32x4){va[u].z, vb[u].z, va[u].w, vb[u].w};
+                }
+            }
         }
         if (tid < 256) cnl[tid] = cn[(int64_t)m * 256 + tid];
         if (tid == 0) ctr[0] = 0;
@@ -585,6 +605,225 @@ __global__ __launch_bounds__(kRWaves * 64) void pq_resolve_cs_kernel(
     }
 }
 
+// Full items (three or more filter candidates inside the window): the filter is re-run for
+// 32 gathered rows at a time — the same f16 operands, accumulator init and window as the
+// encode kernel, but on the unpacked scores — and only the centroids whose score is inside
+// the window get the canonical fp32 chains.  Every minimiser of the canonical score lies
+// inside the window, so the smallest-(s, k) candidate is the canonical code.  Rows the
+// bound cannot vouch for (non-finite, out of range) and rows with more than kFCap
+// candidates are scanned over all 256 centroids.  LDS holds the fp32 codebook (the chains
+// read it; the f16 MFMA operands are converted from it on the fly: f16(tau c), tau = 4 sigma,
+// exactly the prepared image) and, per wave, the 32 fp32 rows and their candidate lists.
+constexpr int kFWaves = 4;
+constexpr int kFCap = 16;
+
+template <int KS>
+constexpr int full_smem_bytes() {
+    return 256 * (16 * KS + 4) * 4 + 256 * 4 + kFWaves * (32 * (16 * KS + 4) * 4 + 32 * kFCap * 4 + 32 * 4);
+}
+
+template <int KS, int V = 0>
+__global__ __launch_bounds__(kFWaves * 64) void pq_resolve_full_kernel(
+    const float* __restrict__ x, int64_t n, int d, int M, int dsub, int64_t rows_per_wg,
+    const float* __restrict__ C, const float* __restrict__ cn, const float* __restrict__ hinit,
+    const float4* __restrict__ bnd, uint8_t* __restrict__ codesT, const uint2* __restrict__ items,
+    const int2* __restrict__ counts) {
+    constexpr int DP = 16 * KS;   // padded dsub
+    constexpr int CP = DP + 4;    // floats per staged centroid row (pad: rows 4 banks apart)
+    constexpr int XP = DP + 4;    // floats per staged x row
+    constexpr int NL = 2 * KS;    // 16-B loads per lane per batch (32 rows of <= DP floats)
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    float* cl = reinterpret_cast<float*>(smem);
+    float* hb = cl + 256 * CP;
+    const int tid = threadIdx.x;
+    const int w = __builtin_amdgcn_readfirstlane(tid >> 6), l = tid & 63;
+    const int r = l & 31, h = l >> 5;
+    float* xf = reinterpret_cast<float*>(reinterpret_cast<unsigned char*>(hb + 256) +
+                                         w * (32 * XP * 4 + 32 * kFCap * 4 + 32 * 4));
+    int* cand = reinterpret_cast<int*>(xf + 32 * XP);
+    int* ccnt = cand + 32 * kFCap;
+
+    int m;
+    int64_t chunk;
+    wg_coords(M, m, chunk);
+    const int64_t r0 = chunk * rows_per_wg;
+    const int64_t r1 = min(n, r0 + rows_per_wg);
+    if (r0 >= r1) return;
+    const int nrows = (int)(r1 - r0);
+    const int nf = counts[blockIdx.x].y;
+    if (nf == 0) return;
+    const float* Cm = C + (int64_t)m * 256 * dsub;
+    {  // 16-B copies, 8 in flight per thread (dsub % 4 == 0 on this path)
+        const int q4 = dsub >> 2, tot = 256 * q4;
+        for (int e0 = tid; e0 < tot; e0 += 8 * kFWaves * 64) {
+            f32x4 v[8];
+#pragma unroll
+            for (int u = 0; u < 8; ++u) {
+                const int e = e0 + u * kFWaves * 64;
+                v[u] = e < tot ? *reinterpret_cast<const f32x4*>(Cm + 4 * (int64_t)e) : (f32x4){0.f, 0.f, 0.f, 0.f};
+            }
+#pragma unroll
+            for (int u = 0; u < 8; ++u) {
+                const int e = e0 + u * kFWaves * 64;
+                const int k = e / q4, j = e - k * q4;
+                if (e < tot) *reinterpret_cast<f32x4*>(cl + k * CP + 4 * j) = v[u];
+            }
+        }
+        for (int e = tid; e < 256 * (DP - dsub); e += kFWaves * 64) {
+            const int k = e / (DP - dsub);
+            cl[k * CP + dsub + (e - k * (DP - dsub))] = 0.0f;
+        }
+    }
+    hb[tid] = hinit[(int64_t)m * 256 + tid];
+    __syncthreads();
+
+    const float4 bm = bnd[m];
+    const float2v sig2 = {bm.x, bm.x};
+    const float2v tau2 = sig2 * (float2v){4.0f, 4.0f};  // 2^kScaleC / 2^kScaleX
+    const float xs_eta = 6.1035156e-5f * sqrtf((float)dsub);
+    const float* cnm = cn + (int64_t)m * 256;
+    const int q = dsub >> 2;
+    const int nld = (32 * q + 63) >> 6;
+    const uint2* list = items + (int64_t)m * n + r0;
+    const float* xsub = x + r0 * d + (int64_t)m * dsub;
+    const int nbat = (nf + 31) >> 5;
+
+    auto frag = [&](const float* src, const float2v sc) __attribute__((always_inline)) {
+        const f32x4 a0 = *reinterpret_cast<const f32x4*>(src);
+        const f32x4 a1 = *reinterpret_cast<const f32x4*>(src + 4);
+        const float2v p0 = (float2v){a0.x, a0.y} * sc, p1 = (float2v){a0.z, a0.w} * sc;
+        const float2v p2 = (float2v){a1.x, a1.y} * sc, p3 = (float2v){a1.z, a1.w} * sc;
+        return (u32x4){cvt2(p0.x, p0.y), cvt2(p1.x, p1.y), cvt2(p2.x, p2.y), cvt2(p3.x, p3.y)};
+    };
+
+    // the A operands of all 8 centroid blocks stay in registers for the whole kernel (one
+    // wave per SIMD: 512 registers per lane)
+    half8 aa[8][KS];
+#pragma unroll
+    for (int cb = 0; cb < 8; ++cb) {
+        const float* crow = cl + (cb * 32 + r) * CP + h * 8 * KS;
+#pragma unroll
+        for (int ks = 0; ks < KS; ++ks) aa[cb][ks] = __builtin_bit_cast(half8, frag(crow + 8 * ks, tau2));
+    }
+
+    for (int b = w; b < nbat; b += kFWaves) {
+        const int first = b * 32;
+        const int cntb = min(32, nf - first);
+        int rowl = 0;
+        if (l < cntb) rowl = (int)list[nrows - 1 - (first + l)].x;
+        // gather the 32 fp32 sub-rows (all loads in flight, then the stores), zero the padding
+        f32x4 v[NL];
+#pragma unroll
+        for (int j = 0; j < NL; ++j) {
+            const int c = j * 64 + l;
+            const int row = c / q, col = c - row * q;
+            const int src = __shfl(rowl, min(row, 31));
+            const bool ok = j < nld && row < cntb && !(V & 4096);
+            v[j] = *reinterpret_cast<const f32x4*>(xsub + (ok ? (int64_t)src * d + 4 * col : 0));
+        }
+#pragma unroll
+        for (int j = 0; j < NL; ++j) {
+            const int c = j * 64 + l;
+            const int row = c / q, col = c - row * q;
+            if (j < nld && row < 32) *reinterpret_cast<f32x4*>(xf + row * XP + 4 * col) = v[j];
+        }
+        for (int e = l; e < 32 * (DP - dsub); e += 64) {
+            const int row = e / (DP - dsub);
+            xf[row * XP + dsub + (e - row * (DP - dsub))] = 0.0f;
+        }
+        if (l < 32) ccnt[l] = 0;
+        lds_fence();
+        // the encode kernel's B operand: lane (r, h) holds x~[r][h*8KS + 8ks + j] = f16(sigma x)
+        half8 bf[KS];
+        float xx = 0.0f;
+#pragma unroll
+        for (int ks = 0; ks < KS; ++ks) {
+            const u32x4 u = frag(xf + r * XP + h * 8 * KS + 8 * ks, sig2);
+            bf[ks] = __builtin_bit_cast(half8, u);
+            xx = dot2_self(u[0], xx); xx = dot2_self(u[1], xx);
+            xx = dot2_self(u[2], xx); xx = dot2_self(u[3], xx);
+        }
+        xx += __shfl_xor(xx, 32);
+        // all 256 unpacked scores of the lane's row half, one MFMA sweep
+        floatx16 acc[8];
+        constexpr int NCB = (V & 2048) ? 1 : 8;
+#pragma unroll
+        for (int cb = 0; cb < NCB; ++cb) {
+#pragma unroll
+            for (int qq = 0; qq < 4; ++qq) {
+                const float4 hv = *reinterpret_cast<const float4*>(hb + cb * 32 + 8 * qq + 4 * h);
+                acc[cb][4 * qq + 0] = hv.x; acc[cb][4 * qq + 1] = hv.y;
+                acc[cb][4 * qq + 2] = hv.z; acc[cb][4 * qq + 3] = hv.w;
+            }
+        }
+#pragma unroll
+        for (int ks = 0; ks < KS; ++ks)
+#pragma unroll
+            for (int cb = 0; cb < NCB; ++cb)
+                acc[cb] = __builtin_amdgcn_mfma_f32_32x32x16_f16(aa[cb][ks], bf[ks], acc[cb], 0, 0, 0);
+        float t1 = -INFINITY;
+#pragma unroll
+        for (int cb = 0; cb < NCB; ++cb)
+#pragma unroll
+            for (int i = 0; i < 16; ++i) t1 = fmaxf(t1, acc[cb][i]);
+        t1 = fmaxf(t1, __shfl_xor(t1, 32));
+        const float Xs = (sqrtf(xx) * (1.0f + 1e-5f) + xs_eta) * (1.0f + 9.765625e-4f);
+        const float W = bm.y * Xs + bm.z;
+        const float thr = t1 - W;
+        const bool bad = !(Xs < 65000.0f) || !isfinite(t1) || !isfinite(W);
+#pragma unroll
+        for (int cb = 0; cb < NCB; ++cb) {
+#pragma unroll
+            for (int i = 0; i < 16; ++i) {
+                if (!bad && acc[cb][i] >= thr) {
+                    const int slot = atomicAdd(&ccnt[r], 1);
+                    if (slot < kFCap) cand[r * kFCap + slot] = cb * 32 + (i & 3) + 8 * (i >> 2) + 4 * h;
+                }
+            }
+        }
+        lds_fence();
+        // canonical chains: lane (r, h) takes every other candidate of row r
+        float bs = INFINITY;
+        int bk = 256;
+        const float* xr = xf + r * XP;
+        auto exact = [&](int k) __attribute__((always_inline)) {
+            const float* c = cl + k * CP;
+            float dot = 0.0f;
+            for (int t = 0; t < dsub; t += 4) {
+                const f32x4 cv = *reinterpret_cast<const f32x4*>(c + t);
+                const f32x4 xv = *reinterpret_cast<const f32x4*>(xr + t);
+                dot = __builtin_fmaf(xv.x, cv.x, dot);
+                dot = __builtin_fmaf(xv.y, cv.y, dot);
+                dot = __builtin_fmaf(xv.z, cv.z, dot);
+                dot = __builtin_fmaf(xv.w, cv.w, dot);
+            }
+            const float sc = __builtin_fmaf(-2.0f, dot, cnm[k]);
+            if (sc < bs || (sc == bs && k < bk)) { bs = sc; bk = k; }
+        };
+        if constexpr ((V & 512) != 0) {  // instrumentation: rows scanned whole, candidates total
+            if (h == 0 && r < cntb) {
+                int2* cc = const_cast<int2*>(counts) + blockIdx.x;
+                if (bad || ccnt[r] > kFCap) atomicAdd(&cc->x, 1 << 16);
+                atomicAdd(&cc->x, 1);
+                atomicAdd(&cc->y, ccnt[r] << 8);
+            }
+        }
+        if (r < cntb && !(V & 1024)) {
+            const int nc = ccnt[r];
+            if (bad || nc > kFCap) {
+                for (int k = h; k < 256; k += 2) exact(k);
+            } else {
+                for (int j = h; j < nc; j += 2) exact(cand[r * kFCap + j]);
+            }
+        }
+        const float os = __shfl_xor(bs, 32);
+        const int ok = __shfl_xor(bk, 32);
+        if (os < bs || (os == bs && ok < bk)) { bs = os; bk = ok; }
+        if (h == 0 && r < cntb) codesT[(int64_t)m * n + r0 + rowl] = (uint8_t)((bs < INFINITY) ? bk : 0);
+        lds_fence();
+    }
+}
+
 // (M, n) -> (n, M): one block per 256 rows, the tile goes through LDS.
 __global__ __launch_bounds__(256) void pq_transpose_codes_kernel(const uint8_t* __restrict__ codesT, int64_t n, int M,
                                                                  uint8_t* __restrict__ codes) {
@@ -661,9 +900,24 @@ hipError_t launch_pq_encode_cs_v(const float* x, int64_t n, int d, int M, int ds
                        static_cast<const half8*>(img), hinit, static_cast<const float4*>(bnd), codesT,
                        static_cast<uint2*>(items), static_cast<int2*>(counts));
     e = hipGetLastError();
-    if (e != hipSuccess || (V & 1)) return e;
+    if (e != hipSuccess || ((V & 1) && !(V & 512))) return e;
+    // full items through pq_resolve_full_kernel (filter re-run + candidate chains): 1.5-2 %
+    // faster end to end than the pair kernel's 256-wide scans (interleaved A/B, 1M x 1536);
+    // V&256 restores the scans
+    constexpr bool mfma_full = (V & 256) == 0;
+    if (mfma_full) {
+        constexpr int fsmem = full_smem_bytes<KS>();
+        auto fkern = pq_resolve_full_kernel<KS, V>;
+        e = hipFuncSetAttribute((const void*)fkern, hipFuncAttributeMaxDynamicSharedMemorySize, fsmem);
+        if (e != hipSuccess) return e;
+        hipLaunchKernelGGL(fkern, dim3((unsigned)grid), dim3(kFWaves * 64), fsmem, st, x, n, d, M, dsub, R, C, cn,
+                           hinit, static_cast<const float4*>(bnd), codesT, static_cast<const uint2*>(items),
+                           static_cast<const int2*>(counts));
+        e = hipGetLastError();
+        if (e != hipSuccess || (V & 1)) return e;  // V&513: the instrumented full kernel alone
+    }
     hipLaunchKernelGGL(rkern, dim3((unsigned)grid), dim3(kRWaves * 64), rsmem, st, x, n, d, M, dsub, R, C, cn, codesT,
-                       static_cast<const uint2*>(items), static_cast<const int2*>(counts));
+                       static_cast<const uint2*>(items), static_cast<const int2*>(counts), mfma_full ? 0 : 1);
     return hipGetLastError();
 }
 

@@ -243,7 +243,13 @@ def test_adc_bit_exact(dev, oracle, nq, n, d, M, nbits, k, metric):
     np.testing.assert_array_equal(_h(ii).view(np.uint32), i_ref)
 
 
-@pytest.mark.parametrize("nq,n,d,k", [(20, 3000, 1024, 10), (7, 500, 37, 100), (4, 3, 16, 5)])
+@pytest.mark.parametrize("nq,n,d,k", [
+    (20, 3000, 1024, 10), (7, 500, 37, 100), (4, 3, 16, 5),    # streaming scan
+    (100, 20000, 96, 10),                                         # tiled, one chunk, 5 segments
+    (4100, 40000, 16, 10),                                        # tiled, 3 chunks + running merge
+    (64, 5000, 30, 100),                                          # tiled, d % 4 != 0
+    (16, 4096, 1536, 256),                                        # tiled, k = 256
+])
 @pytest.mark.parametrize("metric", [1, 0])
 def test_flat_search_bit_exact(dev, oracle, nq, n, d, k, metric):
     from haag_vq import _native
@@ -251,6 +257,9 @@ def test_flat_search_bit_exact(dev, oracle, nq, n, d, k, metric):
     rng = np.random.default_rng(d)
     X = rng.standard_normal((n, d)).astype(np.float32)
     Q = rng.standard_normal((nq, d)).astype(np.float32)
+    if n > 100:
+        X[n - 1] = X[3]      # exact duplicate across segments / chunks: smaller id first
+        X[n // 2] = X[3]
     d_ref, i_ref = oracle.flat_search(Q, X, k, metric)
     dd, ii = _native.flat_search(_t(Q, dev), _t(X, dev), k, metric)
     np.testing.assert_array_equal(_h(dd), d_ref)

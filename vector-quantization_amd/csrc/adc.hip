@@ -428,8 +428,13 @@ hipError_t launch_topk_merge(const float* pd, const uint32_t* pi, int parts, int
 
 using namespace mivq;
 
+// The tiled path (pairwise chains on packed VALU + segmented top-k) wins once there are
+// enough queries to fill a 128-row tile; the streaming scan keeps the small-batch cases.
+static bool flat_use_tiled(int64_t nq, int64_t n) { return nq >= 16 && n >= 4096; }
+
 extern "C" size_t mivq_flat_search_workspace_bytes(int64_t nq, int64_t n, int32_t d, int32_t k) {
     if (nq <= 0 || n <= 0 || d <= 0 || k <= 0) return 0;
+    if (flat_use_tiled(nq, n)) return flat_tiled_workspace_bytes(nq, n, k);
     const int QB = flat_qb(d);
     if (QB == 0) return 0;
     const int64_t parts = adc_chunks(nq, n, QB) * kScanWaves;
@@ -444,7 +449,7 @@ extern "C" int mivq_flat_search(const float* q, int64_t nq, const float* x, int6
     MIVQ_REQUIRE(metric == MIVQ_METRIC_L2 || metric == MIVQ_METRIC_INNER_PRODUCT, MIVQ_ERR_UNSUPPORTED,
                  "flat_search: metric %d", metric);
     const int QB = flat_qb(d);
-    MIVQ_REQUIRE(QB > 0, MIVQ_ERR_UNSUPPORTED, "flat_search: d=%d too large for LDS", d);
+    MIVQ_REQUIRE(QB > 0 || flat_use_tiled(nq, n), MIVQ_ERR_UNSUPPORTED, "flat_search: d=%d too large for LDS", d);
     MIVQ_REQUIRE(id_offset >= 0 && id_offset + n <= (int64_t)kNoId, MIVQ_ERR_INVALID, "flat_search: ids overflow");
     if (nq == 0) return MIVQ_OK;
     hipStream_t st = as_stream(stream);
@@ -458,6 +463,11 @@ extern "C" int mivq_flat_search(const float* q, int64_t nq, const float* x, int6
     const size_t need = mivq_flat_search_workspace_bytes(nq, n, d, k);
     MIVQ_REQUIRE(workspace && workspace_bytes >= need, MIVQ_ERR_WORKSPACE, "flat_search: workspace %zu < %zu",
                  workspace_bytes, need);
+    if (flat_use_tiled(nq, n)) {
+        const hipError_t et = launch_flat_tiled(q, nq, x, n, d, metric, k, id_offset, workspace, dists, ids, st);
+        if (et != hipSuccess) return set_error(MIVQ_ERR_HIP, "flat_search (tiled): %s", hipGetErrorString(et));
+        return MIVQ_OK;
+    }
     const int64_t nch = adc_chunks(nq, n, QB);
     const int parts = (int)(nch * kScanWaves);
     float* pd = static_cast<float*>(workspace);

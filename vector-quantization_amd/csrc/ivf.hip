@@ -418,6 +418,123 @@ __global__ __launch_bounds__(kIvfWaves * 64) void ivfpq_scan_kernel(
     }
 }
 
+// Segmented row top-k for the tiled exact search: the (rows, S*L) block is read as rows*S
+// segments of L columns; segment (row, s) writes its k best (value, base + s*L + col) to part
+// part0 + s of the (parts, rows, k) list layout that topk_merge_kernel consumes.
+template <int R>
+__global__ __launch_bounds__(256) void topk_seg_kernel(const float* __restrict__ dist, int64_t rows, int64_t ld,
+                                                       int64_t ncols, int L, int S, int k, int64_t base,
+                                                       int part0, float* __restrict__ part_d,
+                                                       uint32_t* __restrict__ part_i) {
+    const int lane = threadIdx.x & 63;
+    const int64_t g = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (g >= rows * S) return;
+    const int64_t row = g / S;
+    const int s = (int)(g - row * S);
+    const int64_t c0 = (int64_t)s * L;
+    const int64_t c1 = min<int64_t>(ncols, c0 + L);
+    const float* dr = dist + row * ld;
+    WaveTopK<R> top;
+    top.init();
+    float thr_d = INFINITY;
+    uint32_t thr_i = kNoId;
+    for (int64_t j0 = c0; j0 < c1; j0 += 64) {
+        const int64_t j = j0 + lane;
+        const bool valid = j < c1;
+        float v = valid ? dr[j] : INFINITY;
+        if (v != v) v = INFINITY;
+        top.offer(valid, v, (uint32_t)(base + j), k, lane, thr_d, thr_i);
+    }
+    float* od = part_d + ((int64_t)(part0 + s) * rows + row) * k;
+    uint32_t* oi = part_i + ((int64_t)(part0 + s) * rows + row) * k;
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+        const int e = r * 64 + lane;
+        if (e < k) { od[e] = top.d[r]; oi[e] = top.id[r]; }
+    }
+}
+
+constexpr int kSegL = 4096;
+
+int64_t flat_tiled_cols(int64_t nq, int64_t n) {
+    int64_t bc = ((int64_t)1 << 26) / std::max<int64_t>(nq, 1);  // <= 256 MiB of distances per chunk
+    bc = std::max<int64_t>(kSegL, bc / kSegL * kSegL);
+    return std::min<int64_t>(bc, ceil_div(n, kSegL) * kSegL);
+}
+
+template <int R>
+hipError_t launch_topk_seg(const float* dist, int64_t rows, int64_t ld, int64_t ncols, int S, int k, int64_t base,
+                           int part0, float* pd, uint32_t* pi, hipStream_t st) {
+    hipLaunchKernelGGL(topk_seg_kernel<R>, dim3((unsigned)ceil_div(rows * S, 4)), dim3(256), 0, st, dist, rows, ld,
+                       ncols, kSegL, S, k, base, part0, pd, pi);
+    return hipGetLastError();
+}
+
+}  // namespace
+
+size_t flat_tiled_workspace_bytes(int64_t nq, int64_t n, int k) {
+    const int64_t bc = flat_tiled_cols(nq, n);
+    const int64_t S = bc / kSegL;
+    return align_up((size_t)nq * bc * 4, 256) + 2 * align_up((size_t)(S + 1) * nq * k * 4, 256) +
+           2 * align_up((size_t)nq * k * 4, 256);
+}
+
+// Exact top-k by tiles: pairwise chains for a column chunk, segmented top-k, and a running
+// merge (part 0 = the result so far).  Same chains and (dist, id) order as flat_scan.
+hipError_t launch_flat_tiled(const float* q, int64_t nq, const float* x, int64_t n, int d, int metric, int k,
+                             int64_t id_offset, void* ws, float* dists, uint32_t* ids, hipStream_t st) {
+    const int64_t bc = flat_tiled_cols(nq, n);
+    const int S = (int)(bc / kSegL);
+    unsigned char* p = static_cast<unsigned char*>(ws);
+    float* buf = reinterpret_cast<float*>(p);
+    p += align_up((size_t)nq * bc * 4, 256);
+    float* pd = reinterpret_cast<float*>(p);
+    p += align_up((size_t)(S + 1) * nq * k * 4, 256);
+    uint32_t* pi = reinterpret_cast<uint32_t*>(p);
+    p += align_up((size_t)(S + 1) * nq * k * 4, 256);
+    float* rd = reinterpret_cast<float*>(p);
+    p += align_up((size_t)nq * k * 4, 256);
+    uint32_t* ri = reinterpret_cast<uint32_t*>(p);
+    const bool vec = (d % 4) == 0 && ((uintptr_t)q % 16) == 0 && ((uintptr_t)x % 16) == 0;
+    const bool ip = metric == MIVQ_METRIC_INNER_PRODUCT;
+    hipError_t e = hipSuccess;
+    int nparts = 0;  // parts holding data in pd/pi (part 0 = running result once set)
+    for (int64_t c0 = 0; c0 < n; c0 += bc) {
+        const int64_t m = std::min<int64_t>(bc, n - c0);
+        const dim3 grid((unsigned)ceil_div(nq, PBM), (unsigned)ceil_div(m, PBN));
+        const float* y = x + c0 * d;
+        if (ip) {
+            if (vec) hipLaunchKernelGGL((pairwise_kernel<true, true>), grid, dim3(256), 0, st, q, nq, y, m, d, buf);
+            else hipLaunchKernelGGL((pairwise_kernel<true, false>), grid, dim3(256), 0, st, q, nq, y, m, d, buf);
+        } else {
+            if (vec) hipLaunchKernelGGL((pairwise_kernel<false, true>), grid, dim3(256), 0, st, q, nq, y, m, d, buf);
+            else hipLaunchKernelGGL((pairwise_kernel<false, false>), grid, dim3(256), 0, st, q, nq, y, m, d, buf);
+        }
+        const int Sc = (int)ceil_div(m, kSegL);
+        const int part0 = nparts == 0 ? 0 : 1;
+        switch ((k + 63) / 64) {
+            case 1: e = launch_topk_seg<1>(buf, nq, m, m, Sc, k, id_offset + c0, part0, pd, pi, st); break;
+            case 2: e = launch_topk_seg<2>(buf, nq, m, m, Sc, k, id_offset + c0, part0, pd, pi, st); break;
+            case 3: e = launch_topk_seg<3>(buf, nq, m, m, Sc, k, id_offset + c0, part0, pd, pi, st); break;
+            default: e = launch_topk_seg<4>(buf, nq, m, m, Sc, k, id_offset + c0, part0, pd, pi, st); break;
+        }
+        if (e != hipSuccess) return e;
+        nparts = part0 + Sc;
+        const bool last = c0 + bc >= n;
+        e = launch_topk_merge(pd, pi, nparts, nq, k, last ? dists : rd, last ? ids : ri, st);
+        if (e != hipSuccess) return e;
+        if (!last) {  // the merged list becomes part 0
+            e = hipMemcpyAsync(pd, rd, (size_t)nq * k * 4, hipMemcpyDeviceToDevice, st);
+            if (e == hipSuccess) e = hipMemcpyAsync(pi, ri, (size_t)nq * k * 4, hipMemcpyDeviceToDevice, st);
+            if (e != hipSuccess) return e;
+            nparts = 1;
+        }
+    }
+    return e;
+}
+
+namespace {
+
 int ivf_splits(int64_t nq, int nprobe) {
     const int64_t want = ceil_div(512, std::max<int64_t>(nq, 1));
     const int64_t maxs = ceil_div(nprobe, kIvfWaves);

@@ -82,4 +82,9 @@ struct WaveTopK {
 hipError_t launch_topk_merge(const float* pd, const uint32_t* pi, int parts, int64_t nq, int k, float* od,
                              uint32_t* oi, hipStream_t st);
 
+// Tiled exact brute force (ivf.hip): pairwise chains + segmented top-k + running merge.
+size_t flat_tiled_workspace_bytes(int64_t nq, int64_t n, int k);
+hipError_t launch_flat_tiled(const float* q, int64_t nq, const float* x, int64_t n, int d, int metric, int k,
+                             int64_t id_offset, void* ws, float* dists, uint32_t* ids, hipStream_t st);
+
 }  // namespace mivq

@@ -19,13 +19,15 @@ step() {  # step <name> <seconds> <cmd...>
     fi
     return 0
 }
+i=0
 for s in "$@"; do
+    i=$((i+1))
     case "$s" in
         smoke)   step smoke 400 python -c "import __graft_entry__ as g; g.smoke()" ;;
         pytest)  step pytest 900 python -m pytest tests -m gpu -q -rf ;;
         bench)   step bench 600 python bench.py --steps 10 --warmup 3 ;;
         prof)    step prof 600 rocprofv3 --kernel-trace --stats -d $OUT/prof -o run --output-format csv -- python bench.py --steps 5 --warmup 2 --no-cpu-baseline ;;
-        *)       step custom 600 bash -c "$s" ;;
+        *)       step "custom$i" 600 bash -c "$s" ;;
     esac
 done
 echo "=== session done $(date +%T)" | tee -a $OUT/session.log

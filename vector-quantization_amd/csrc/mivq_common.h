@@ -36,8 +36,9 @@ inline size_t align_up(size_t v, size_t a) { return (v + a - 1) / a * a; }
 //           dsub padded to KS*16), see pq_encode.hip
 //   hinit : (M, ksub)           f32  -||c||^2 / 2 * scale^2 (MFMA accumulator init)
 //   bnd   : (M, 4)              f32  per-subspace constants of the filter error bound
+//   spread: (M, 2)              u32  bits of Dmax, DDmax (pairwise spreads of the image)
 struct PqPrepLayout {
-    size_t cn, ct, img, hinit, bnd, total;
+    size_t cn, ct, img, hinit, bnd, spread, total;
     int32_t dsub, ksub, ks;  // ks = padded dsub / 16 (k-steps of the f16 MFMA)
     bool mfma;               // filter path available for this shape
 };
@@ -54,6 +55,7 @@ inline PqPrepLayout pq_prep_layout(int32_t d, int32_t M, int32_t nbits) {
     L.img = off;   off = align_up(off + (L.mfma ? (size_t)M * 8 * L.ks * 64 * 8 * 2 : 0), 256);
     L.hinit = off; off = align_up(off + sizeof(float) * (size_t)M * L.ksub, 256);
     L.bnd = off;   off = align_up(off + sizeof(float) * (size_t)M * 4, 256);
+    L.spread = off; off = align_up(off + sizeof(uint32_t) * (size_t)M * 2, 256);
     L.total = off;
     return L;
 }

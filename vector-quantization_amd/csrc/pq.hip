@@ -54,34 +54,79 @@ constexpr float kPack = 3.0517578e-5f;   // 2^-15: 8 low mantissa bits replaced 
 constexpr int kScaleC = 14;              // max |c~| <= 2^14
 constexpr int kScaleX = 12;              // |x~| < 65504 while |x| < 2^4 * 2^ceil(log2 max|c|)
 
+// Scale exponent of subspace m: e = ceil(log2 max|c|) (clamped), tau = 2^(kScaleC - e),
+// sigma = 2^(kScaleX - e).  Block-wide (256 threads); `red` is 256 floats of LDS.
+__device__ int subspace_scale_exp(const float* Cm, int dsub, float* red) {
+    const int tid = threadIdx.x;
+    float mabs = 0.0f;
+    for (int t = 0; t < dsub; ++t) mabs = fmaxf(mabs, fabsf(Cm[(int64_t)tid * dsub + t]));
+    red[tid] = mabs;
+    __syncthreads();
+    for (int s = 128; s > 0; s >>= 1) {
+        if (tid < s) red[tid] = fmaxf(red[tid], red[tid + s]);
+        __syncthreads();
+    }
+    const float cmax_abs = red[0];
+    __syncthreads();
+    int e = 0;
+    if (cmax_abs > 0.0f && isfinite(cmax_abs)) e = (int)ceilf(log2f(cmax_abs));
+    return max(-100, min(100, e));
+}
+
+// Pairwise spreads of the prepared image of subspace m (the window derivation above
+// pq_encode_mfma_kernel):  Dmax = max_ij ||c~_i - c~_j||,  DDmax = max_ij ||dc_i - dc_j||,
+// c~ = f16(tau c), dc = c~ - tau c (exact in fp32).  Grid (M, 16): block (m, g) takes rows
+// i in [16g, 16g + 16) against all 256 j, one fp32 chain per pair (relative rounding of a
+// squared sum <= (dsub + 3) 2^-24, covered by the (1 + 1e-5) applied to the norms); the
+// maxima of the squared sums go to spread[m] with atomicMax on their bits (non-negative).
+__global__ __launch_bounds__(256) void pq_prep_spread_kernel(const float* __restrict__ C, int dsub,
+                                                             uint32_t* __restrict__ spread) {
+    __shared__ float red[256];
+    const int m = blockIdx.x, g = blockIdx.y, tid = threadIdx.x;
+    const float* Cm = C + (int64_t)m * 256 * dsub;
+    const float tau = ldexpf(1.0f, kScaleC - subspace_scale_exp(Cm, dsub, red));
+    const int i = 16 * g + (tid >> 4);
+    const float* ci = Cm + (int64_t)i * dsub;
+    float d1 = 0.0f, d2 = 0.0f;
+    for (int jj = 0; jj < 16; ++jj) {
+        const float* cj = Cm + (int64_t)(16 * jj + (tid & 15)) * dsub;
+        float s1 = 0.0f, s2 = 0.0f;
+        for (int t = 0; t < dsub; ++t) {
+            const float ti = tau * ci[t], tj = tau * cj[t];
+            const float hi = (float)(_Float16)ti, hj = (float)(_Float16)tj;
+            const float dc = (hi - ti) - (hj - tj);
+            const float dh = hi - hj;
+            s1 = __builtin_fmaf(dh, dh, s1);
+            s2 = __builtin_fmaf(dc, dc, s2);
+        }
+        // NaN pairs (a NaN centroid never wins, and its filter score is never a candidate)
+        // are skipped by fmaxf; inf gives inf -> the window is infinite
+        d1 = fmaxf(d1, s1);
+        d2 = fmaxf(d2, s2);
+    }
+    atomicMax(&spread[2 * m + 0], __float_as_uint(d1));
+    atomicMax(&spread[2 * m + 1], __float_as_uint(d2));
+}
+
 // One block (256 threads) per subspace m: scales, the f16 operand image, the scaled
 // accumulator init and the bound constants.  See the derivation at pq_encode_mfma.
 __global__ void pq_prep_mfma_kernel(const float* __restrict__ C, const float* __restrict__ cn,
                                     int M, int dsub, int KS, half8* __restrict__ img,
-                                    float* __restrict__ hinit, float4* __restrict__ bnd) {
+                                    float* __restrict__ hinit, float4* __restrict__ bnd,
+                                    const uint32_t* __restrict__ spread) {
     const int m = blockIdx.x;
     const int tid = threadIdx.x;  // 256 threads
-    __shared__ float red_abs[256];
     __shared__ float red_nrm[256];
     const float* Cm = C + (int64_t)m * 256 * dsub;
-    // max |c| and max ||c|| over the subspace
-    float mabs = 0.0f;
-    for (int t = 0; t < dsub; ++t) mabs = fmaxf(mabs, fabsf(Cm[(int64_t)tid * dsub + t]));
-    red_abs[tid] = mabs;
+    const int e = subspace_scale_exp(Cm, dsub, red_nrm);
+    // max ||c||^2 over the subspace
     red_nrm[tid] = cn[(int64_t)m * 256 + tid];
     __syncthreads();
     for (int s = 128; s > 0; s >>= 1) {
-        if (tid < s) {
-            red_abs[tid] = fmaxf(red_abs[tid], red_abs[tid + s]);
-            red_nrm[tid] = fmaxf(red_nrm[tid], red_nrm[tid + s]);
-        }
+        if (tid < s) red_nrm[tid] = fmaxf(red_nrm[tid], red_nrm[tid + s]);
         __syncthreads();
     }
-    const float cmax_abs = red_abs[0];
     const float cn_max = red_nrm[0];
-    int e = 0;
-    if (cmax_abs > 0.0f && isfinite(cmax_abs)) e = (int)ceilf(log2f(cmax_abs));
-    e = max(-100, min(100, e));
     const float tau = ldexpf(1.0f, kScaleC - e);  // c~ = f16(tau * c)
     const float sigma = ldexpf(1.0f, kScaleX - e);  // x~ = f16(sigma * x)
     const float st = sigma * tau;
@@ -106,14 +151,14 @@ __global__ void pq_prep_mfma_kernel(const float* __restrict__ C, const float* __
     if (tid == 0) {
         // Window W(Xs) = a * Xs + b in accumulator units; Xs = sigma * ||x_m||, Cs = tau * Cmax.
         const float Cs = tau * sqrtf(cn_max) * (1.0f + 1e-6f);
+        const float Dm = sqrtf(__uint_as_float(spread[2 * m + 0])) * (1.0f + 1e-5f);
+        const float DDm = sqrtf(__uint_as_float(spread[2 * m + 1])) * (1.0f + 1e-5f);
         const float gd = (float)dsub * kU32 / (1.0f - (float)dsub * kU32);
         const float gn = (float)(dsub + 2) * kU32 / (1.0f - (float)(dsub + 2) * kU32);
         const float sq = sqrtf((float)dsub);
-        const float a = Cs * (4.0f * kUh + 2.0f * kUh * kUh + 2.004f * gn + 2.004f * kPack + gd + kU32)
-                      + 2.0f * kEta * sq;
-        const float b = Cs * Cs * (gn + 1.5f * gd + kPack + 0.5f * kU32) + 2.002f * kEta * sq * Cs
-                      + 2.0f * (float)dsub * kEta * kEta;
-        const bool ok = isfinite(Cs) && isfinite(a) && isfinite(b);
+        const float a = kUh * Dm + DDm + Cs * (2.004f * gn + 2.004f * kPack + 2.0f * (gd + kU32));
+        const float b = 1.001f * kEta * sq * Dm + Cs * Cs * (gn + 2.0f * gd + kPack + kU32);
+        const bool ok = isfinite(Cs) && isfinite(a) && isfinite(b) && isfinite(Dm) && isfinite(DDm);
         bnd[m] = make_float4(sigma, ok ? a * 1.0625f : INFINITY, ok ? b * 1.0625f + 1e-30f : INFINITY, Cs);
     }
 }
@@ -165,14 +210,17 @@ __global__ __launch_bounds__(64) void pq_encode_exact_kernel(
 
 // ------------------------------------------------------------------------- MFMA encode
 // Error window (all in accumulator units, i.e. scaled by sigma*tau; a_k = <x,c_k> - |c_k|^2/2
-// is maximised, Xs = sigma*||x_m||, Cs = tau*max_k ||c_k||):
-//   filter  |p_k - st*a_k| <= E = (2u_h+u_h^2) Xs Cs + eta sqrt(dsub) (Xs + 1.001 Cs)
-//                                 + dsub eta^2 + g_{dsub+2} (Cs^2/2 + 1.002 Xs Cs)
-//                                 + g_dsub Cs^2/2 + 2^-15 (Cs^2/2 + 1.002 Xs Cs)
-//     (f16 rounding of x and c, f16 denormals/flush, fp32 accumulation in any order,
-//      rounding of cn, and the 8 index bits packed into the mantissa)
+// is maximised, Xs >= sigma*||x_m||, Cs = tau*max_k ||c_k||, x~ = f16(sigma x), c~_k = f16(tau c_k),
+// dx = x~ - sigma x, dc_k = c~_k - tau c_k).  For the canonical winner k* and any k, the
+// f16 rounding enters the DIFFERENCE of the two filter scores only as
+//     <dx, c~_k - c~_k*> + <sigma x, dc_k - dc_k*>  <=  ||dx|| Dmax + Xs DDmax,
+//     ||dx|| <= u_h Xs + eta sqrt(dsub)   (f16 rounding, denormals/flush),
+// with Dmax = max_ij ||c~_i - c~_j|| and DDmax = max_ij ||dc_i - dc_j|| measured on the
+// prepared image (pq_prep_mfma_kernel).  Per score, on top of that:
+//   E' = g_{dsub+2} (Cs^2/2 + 1.002 Xs Cs) + g_dsub Cs^2/2 + 2^-15 (Cs^2/2 + 1.002 Xs Cs)
+//     (fp32 accumulation in any order, rounding of cn, the 8 index bits packed into the mantissa)
 //   canonical  |st*A_k - st*a_k| <= G/2 with G = (g_dsub + u) (Cs^2 + 2 Xs Cs)
-//   => the canonical winner k* satisfies p_{k*} >= p_max - (2E + G).
+//   => p_{k*} >= p_max - (||dx|| Dmax + Xs DDmax + 2E' + G).
 // W = a*Xs + b (pq_prep_mfma_kernel) includes a 1.0625 safety factor.
 constexpr int kWaves = 8;  // 512 threads: 2 waves per SIMD, 256 rows per workgroup
 
@@ -573,10 +621,15 @@ extern "C" int mivq_pq_prepare(const float* centroids, int32_t d, int32_t M, int
     int rc = check_launch("pq_prep_norms");
     if (rc) return rc;
     if (L.mfma) {
+        uint32_t* spread = reinterpret_cast<uint32_t*>(p + L.spread);
+        if (hipMemsetAsync(spread, 0, sizeof(uint32_t) * 2 * (size_t)M, st) != hipSuccess) return check_launch("pq_prep_spread");
+        hipLaunchKernelGGL(pq_prep_spread_kernel, dim3(M, 16), dim3(256), 0, st, centroids, L.dsub, spread);
+        rc = check_launch("pq_prep_spread");
+        if (rc) return rc;
         hipLaunchKernelGGL(pq_prep_mfma_kernel, dim3(M), dim3(256), 0, st, centroids,
                            reinterpret_cast<const float*>(p + L.cn), M, L.dsub, L.ks,
                            reinterpret_cast<half8*>(p + L.img), reinterpret_cast<float*>(p + L.hinit),
-                           reinterpret_cast<float4*>(p + L.bnd));
+                           reinterpret_cast<float4*>(p + L.bnd), spread);
         rc = check_launch("pq_prep_mfma");
     }
     return rc;

@@ -128,8 +128,7 @@ __device__ __forceinline__ void lds_burst(uint32_t xa, uint32_t ca, f32x4 (&xq)[
 // the grid allows, each XCD gets all M subspaces of a chunk in consecutive slots, so the M
 // workgroups reading one row range run side by side on one XCD and sweep the same DRAM pages
 // together.  Both kernels of the encode use the same mapping (the lists are per workgroup).
-__device__ __forceinline__ void wg_coords(int M, int& m, int64_t& chunk) {
-    const unsigned b = blockIdx.x, g = gridDim.x;
+__device__ __forceinline__ void wg_coords_of(unsigned b, unsigned g, int M, int& m, int64_t& chunk) {
     if (g % (8u * (unsigned)M) == 0) {
         const unsigned j = b >> 3;
         m = (int)(j % (unsigned)M);
@@ -138,6 +137,10 @@ __device__ __forceinline__ void wg_coords(int M, int& m, int64_t& chunk) {
         m = (int)(b % (unsigned)M);
         chunk = b / (unsigned)M;
     }
+}
+
+__device__ __forceinline__ void wg_coords(int M, int& m, int64_t& chunk) {
+    wg_coords_of(blockIdx.x, gridDim.x, M, m, chunk);
 }
 
 // Load instructions per vb: ceil(32 / RPI), RPI = floor(64 / (dsub/4)) >= floor(16 / KS).

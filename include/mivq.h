@@ -130,6 +130,20 @@ int mivq_rabitq_encode(const float* x, int64_t n, int32_t d, const float* centro
                        int32_t metric, uint8_t* codes, void* stream);
 int mivq_rabitq_decode(const uint8_t* codes, int64_t n, int32_t d, const float* centroid,
                        float* out, void* stream);
+/* RaBitQ estimator search: replaces faiss.IndexRaBitQ.search behind RaBitQIndex
+ * (methods/search/rabitq_index.py:42-70; qb = IndexRaBitQ.qb query bits, 0..8).  codes: (n,
+ * code_size) rows from mivq_rabitq_encode with the same centroid (IndexRaBitQ's center);
+ * q: (nq, d) f32.  Per query r = q - c is quantised to qb bits (min/max grid, round half up);
+ * the estimate of ||q - x||^2 is  f0 + ||r||^2 - 2 f1 <r', bits>-term  (arithmetic:
+ * oracle/mivq_oracle.c oracle_rabitq_est).  dists/ids: (nq, k) ascending keys, ties to the
+ * smaller id; L2 keys are the distance estimates, INNER_PRODUCT keys the negated
+ * inner-product estimates.  ids = id_offset + row.  Workspace from
+ * mivq_rabitq_search_workspace_bytes. */
+size_t mivq_rabitq_search_workspace_bytes(int64_t nq, int64_t n, int32_t d, int32_t k);
+int mivq_rabitq_search(const uint8_t* codes, int64_t n, int32_t d, const float* centroid,
+                       const float* q, int64_t nq, int32_t qb, int32_t metric, int32_t k,
+                       int64_t id_offset, void* workspace, size_t workspace_bytes, float* dists,
+                       uint32_t* ids, void* stream);
 
 /* ------------------------------------------------------ Extended RaBitQ (B bits)
  * The element-wise / per-row steps of ExtendedRaBitQuantizer.compress / decompress

@@ -241,6 +241,18 @@ def rabitq_decode(codes: np.ndarray, d: int, centroid=None) -> np.ndarray:
 
 
 # ----------------------------------------------------------------------------- Extended RaBitQ
+def rabitq_est(codes: np.ndarray, d: int, Q: np.ndarray, centroid=None, qb: int = 4, metric: int = 1) -> np.ndarray:
+    """RaBitQ estimator keys (nq, n) of IndexRaBitQ search (see oracle_rabitq_est); ascending ranks best."""
+    codes = np.ascontiguousarray(codes, dtype=np.uint8)
+    Q = np.ascontiguousarray(Q, dtype=np.float32)
+    c = None if centroid is None else np.ascontiguousarray(centroid, dtype=np.float32)
+    nq, n = Q.shape[0], codes.shape[0]
+    out = np.empty((nq, n), np.float32)
+    lib().oracle_rabitq_est(_p(codes), _i64(n), _i32(d), _p(Q), _i64(nq), None if c is None else _p(c),
+                            _i32(qb), _i32(metric), _p(out))
+    return out
+
+
 def lloyd_1d_normal(num_levels: int, seed: int, n_samples: int = 200_000,
                     max_iter: int = 100, tol: float = 1e-7) -> np.ndarray:
     """Restates extended_rabitq.py:6-44 (1-D Lloyd on an N(0,1) sample)."""

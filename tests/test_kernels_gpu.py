@@ -331,3 +331,31 @@ def test_kmeans_update_deterministic(dev):
                 np.testing.assert_array_equal(C[m, k], (s / np.float32(sel.sum())).astype(np.float32))
             else:
                 np.testing.assert_array_equal(C[m, k], C0[m, k])
+
+
+@pytest.mark.parametrize("nq,n,d,qb,k", [
+    (37, 3000, 1536, 4, 10),    # MFMA path, the RaBitQIndex default qb
+    (40, 1000, 256, 8, 17),     # qb = 8: int8 offset 128
+    (33, 777, 96, 1, 5),        # qb = 1, ragged tiles
+    (9, 500, 100, 4, 10),       # d % 32 != 0: generic kernel
+    (5, 300, 64, 0, 8),         # qb = 0: float estimator (generic kernel)
+    (3, 5, 64, 4, 10),          # fewer codes than k: sentinel slots
+    (16500, 8500, 32, 4, 3),    # three column chunks of the tiled top-k
+])
+@pytest.mark.parametrize("metric", [1, 0])
+def test_rabitq_search_bit_exact(dev, oracle, nq, n, d, qb, k, metric):
+    from haag_vq import _native
+
+    rng = np.random.default_rng(nq + n + d + qb)
+    X = rng.standard_normal((n, d)).astype(np.float32)
+    X[n // 2] = X[n // 3]  # duplicate code: tie broken by the smaller id
+    Q = rng.standard_normal((nq, d)).astype(np.float32)
+    Q[0] = 0.25  # constant query residual -> delta = 0 guard
+    c = X.mean(0).astype(np.float32)
+    cd = _t(c, dev)
+    codes = _native.rabitq_encode(_t(X, dev), cd, metric)
+    kd, ki = _native.rabitq_search(codes, d, cd, _t(Q, dev), qb, metric, k)
+    keys = oracle.rabitq_est(_h(codes), d, Q, c, qb, metric)
+    rd, ri = oracle.topk_rows(keys, k)
+    np.testing.assert_array_equal(_h(ki).view(np.uint32), ri)
+    np.testing.assert_array_equal(_h(kd), rd)

@@ -159,3 +159,33 @@ def test_bucket_sort_oracle_is_stable(oracle):
     off, order = oracle.bucket_sort(a, 5)
     assert off.tolist() == [0, 1, 3, 3, 6, 6]
     assert order.tolist() == [3, 1, 4, 0, 2, 5]
+
+
+def test_rabitq_estimator_restatement_matches_fp64_formula():
+    """oracle_rabitq_est (qb = 0) equals the RaBitQ estimator written out in fp64:
+    ||r||^2 + ||q - c||^2 - 2 f1 <q - c, (2b - 1)/sqrt(d)>, and qb = 8 stays close to it."""
+    import oracle as O
+
+    rng = np.random.default_rng(5)
+    n, nq, d = 200, 7, 64
+    X = rng.standard_normal((n, d)).astype(np.float32)
+    Q = rng.standard_normal((nq, d)).astype(np.float32)
+    c = X.mean(0).astype(np.float32)
+    codes = O.rabitq_encode(X, c, metric=1)
+    nb = d // 8
+    bits = np.unpackbits(codes[:, :nb], axis=1, bitorder="little")[:, :d].astype(np.float64)
+    f = codes[:, nb:].copy().view(np.float32).astype(np.float64)
+    r = (Q - c).astype(np.float64)
+    want = f[None, :, 0] + (r ** 2).sum(1)[:, None] - 2 * f[None, :, 1] * (r @ (2 * bits - 1).T) / np.sqrt(d)
+    got0 = O.rabitq_est(codes, d, Q, c, qb=0, metric=1)
+    np.testing.assert_allclose(got0, want, rtol=1e-4, atol=1e-3)
+    got8 = O.rabitq_est(codes, d, Q, c, qb=8, metric=1)
+    assert np.abs(got8 - want).max() < 0.05 * np.abs(want).max()
+    # IP keys are the negated inner-product estimates 0.5 (pre - ||q||^2), f0 = ||r||^2 - ||x||^2
+    codes_ip = O.rabitq_encode(X, c, metric=0)
+    f_ip = codes_ip[:, nb:].copy().view(np.float32).astype(np.float64)
+    pre = f_ip[None, :, 0] + (r ** 2).sum(1)[:, None] - 2 * f_ip[None, :, 1] * (r @ (2 * bits - 1).T) / np.sqrt(d)
+    want_ip = 0.5 * (pre - (Q.astype(np.float64) ** 2).sum(1)[:, None])
+    ip = O.rabitq_est(codes_ip, d, Q, c, qb=0, metric=0)
+    np.testing.assert_allclose(ip, want_ip, rtol=1e-4, atol=1e-3)
+    assert np.corrcoef(ip.ravel(), -(Q @ X.T).ravel())[0, 1] > 0.6  # 1-bit codes, d = 64

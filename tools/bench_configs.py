@@ -6,7 +6,8 @@ usage: python tools/bench_configs.py --workload opq32|sq8|rabitq1|ivfpq [--n N] 
           and ADC recall@10 / queries/s (queries rotated, LUT + scan), OPQ trained on 65,536 rows.
   sq8     configs[3]: SQ-8 encode of 1M x 3072 (fit = per-dim min/max), and search by decode +
           exact scan (the reference's SQ search) for 100 queries.
-  rabitq1 configs[3]: RaBitQ 1-bit encode of 1M x 3072, search by decode + exact scan.
+  rabitq1 configs[3]: RaBitQ 1-bit encode of 1M x 3072, search by decode + exact scan, and the
+          RaBitQIndex estimator search (qb 4) for --nq queries.
   ivfpq   SURVEY §8f rank 2: FaissIvfPqIndex defaults (K 4096, m 16, nbits 8, nprobe 200)
           over 1M x 1536: build (coarse k-means + residual PQ + add) time, search queries/s
           and recall@10 against exact ground truth.
@@ -130,6 +131,21 @@ def run_flatcodes(a, dev, kind):
     _, gi = _native.flat_search(Q, X, 10)
     rec = recall(gi.cpu().numpy(), ai.cpu().numpy(), 10)
     ach = a.n * bytes_per / (dev_ms * 1e-3) / 1e9
+    est = None
+    if kind == "rabitq1":  # RaBitQIndex: IndexRaBitQ estimator search (center = mean, qb = 4)
+        center = X.double().mean(0).float().contiguous()
+        codes_c = _native.rabitq_encode(X, center, _native.METRIC_L2)
+        Qe = X[: a.nq].contiguous()
+
+        def est_search():
+            return _native.rabitq_search(codes_c, d, center, Qe, 4, _native.METRIC_L2, 10)
+
+        ewall, edev = timed(est_search, 3, 1)
+        _, ei = est_search()
+        est = {"qps": a.nq / ewall, "nq": a.nq, "k": 10, "qb": 4, "ms_per_batch": ewall * 1e3,
+               "recall@10": recall(gi.cpu().numpy(), ei[:100].cpu().numpy(), 10),
+               "codes_bytes": int(codes_c.numel()),
+               "method": "mivq_rabitq_search: int8 MFMA over sign bits + estimator + tiled top-k"}
     return {
         "metric": f"{kind} encode vectors/sec + search queries/sec @ recall@10, 1M×3072 fp32 (BASELINE configs[3])",
         "value": a.n / wall, "unit": "vectors/s", "ms_per_step": wall * 1e3, "dtype": "f32",
@@ -138,6 +154,7 @@ def run_flatcodes(a, dev, kind):
                      "frac": ach / HBM_PEAK_GBS, "bytes_per_vector": bytes_per, "kernel_ms": dev_ms},
         "search": {"qps": 100 / swall, "nq": 100, "k": 10, "recall@10": rec,
                    "method": "decode + exact L2 scan of the reconstructions (reference flat search)"},
+        "estimator_search": est,
     }
 
 

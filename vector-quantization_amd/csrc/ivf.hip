@@ -479,10 +479,11 @@ size_t flat_tiled_workspace_bytes(int64_t nq, int64_t n, int k) {
            2 * align_up((size_t)nq * k * 4, 256);
 }
 
-// Exact top-k by tiles: pairwise chains for a column chunk, segmented top-k, and a running
-// merge (part 0 = the result so far).  Same chains and (dist, id) order as flat_scan.
-hipError_t launch_flat_tiled(const float* q, int64_t nq, const float* x, int64_t n, int d, int metric, int k,
-                             int64_t id_offset, void* ws, float* dists, uint32_t* ids, hipStream_t st) {
+// Top-k by tiles: `tile(c0, m, buf)` writes the (nq, m) key block of columns [c0, c0 + m)
+// (row stride m) into buf; a segmented top-k and a running merge (part 0 = the result so
+// far) follow each block.  Keys rank ascending, ties by the smaller id.
+hipError_t launch_tiled_topk(int64_t nq, int64_t n, int k, int64_t id_offset, void* ws, float* dists,
+                             uint32_t* ids, hipStream_t st, const TileFn& tile) {
     const int64_t bc = flat_tiled_cols(nq, n);
     const int S = (int)(bc / kSegL);
     unsigned char* p = static_cast<unsigned char*>(ws);
@@ -495,21 +496,12 @@ hipError_t launch_flat_tiled(const float* q, int64_t nq, const float* x, int64_t
     float* rd = reinterpret_cast<float*>(p);
     p += align_up((size_t)nq * k * 4, 256);
     uint32_t* ri = reinterpret_cast<uint32_t*>(p);
-    const bool vec = (d % 4) == 0 && ((uintptr_t)q % 16) == 0 && ((uintptr_t)x % 16) == 0;
-    const bool ip = metric == MIVQ_METRIC_INNER_PRODUCT;
     hipError_t e = hipSuccess;
     int nparts = 0;  // parts holding data in pd/pi (part 0 = running result once set)
     for (int64_t c0 = 0; c0 < n; c0 += bc) {
         const int64_t m = std::min<int64_t>(bc, n - c0);
-        const dim3 grid((unsigned)ceil_div(nq, PBM), (unsigned)ceil_div(m, PBN));
-        const float* y = x + c0 * d;
-        if (ip) {
-            if (vec) hipLaunchKernelGGL((pairwise_kernel<true, true>), grid, dim3(256), 0, st, q, nq, y, m, d, buf);
-            else hipLaunchKernelGGL((pairwise_kernel<true, false>), grid, dim3(256), 0, st, q, nq, y, m, d, buf);
-        } else {
-            if (vec) hipLaunchKernelGGL((pairwise_kernel<false, true>), grid, dim3(256), 0, st, q, nq, y, m, d, buf);
-            else hipLaunchKernelGGL((pairwise_kernel<false, false>), grid, dim3(256), 0, st, q, nq, y, m, d, buf);
-        }
+        e = tile(c0, m, buf);
+        if (e != hipSuccess) return e;
         const int Sc = (int)ceil_div(m, kSegL);
         const int part0 = nparts == 0 ? 0 : 1;
         switch ((k + 63) / 64) {
@@ -531,6 +523,26 @@ hipError_t launch_flat_tiled(const float* q, int64_t nq, const float* x, int64_t
         }
     }
     return e;
+}
+
+// Exact top-k by tiles: pairwise chains for a column chunk, then launch_tiled_topk's
+// segmented top-k and running merge.  Same chains and (dist, id) order as flat_scan.
+hipError_t launch_flat_tiled(const float* q, int64_t nq, const float* x, int64_t n, int d, int metric, int k,
+                             int64_t id_offset, void* ws, float* dists, uint32_t* ids, hipStream_t st) {
+    const bool vec = (d % 4) == 0 && ((uintptr_t)q % 16) == 0 && ((uintptr_t)x % 16) == 0;
+    const bool ip = metric == MIVQ_METRIC_INNER_PRODUCT;
+    return launch_tiled_topk(nq, n, k, id_offset, ws, dists, ids, st, [&](int64_t c0, int64_t m, float* buf) {
+        const dim3 grid((unsigned)ceil_div(nq, PBM), (unsigned)ceil_div(m, PBN));
+        const float* y = x + c0 * d;
+        if (ip) {
+            if (vec) hipLaunchKernelGGL((pairwise_kernel<true, true>), grid, dim3(256), 0, st, q, nq, y, m, d, buf);
+            else hipLaunchKernelGGL((pairwise_kernel<true, false>), grid, dim3(256), 0, st, q, nq, y, m, d, buf);
+        } else {
+            if (vec) hipLaunchKernelGGL((pairwise_kernel<false, true>), grid, dim3(256), 0, st, q, nq, y, m, d, buf);
+            else hipLaunchKernelGGL((pairwise_kernel<false, false>), grid, dim3(256), 0, st, q, nq, y, m, d, buf);
+        }
+        return hipGetLastError();
+    });
 }
 
 namespace {

@@ -157,9 +157,11 @@ constexpr int max_loads() {
 // items with the pair kernel's 256-wide exact scans instead of pq_resolve_full_kernel, 512
 // makes that kernel count (into `counts`) its rows, whole-row scans and candidates; with 512:
 // 1024 skips its exact chains, 2048 runs one filter block, 4096 gathers row 0 only.
-template <int KS, int LAYOUT, int V = 0>
+// DS > 0: the kernel for sub-rows of exactly DS floats (the addresses and load counts fold
+// to constants); DS = 0 reads dsub at run time.
+template <int KS, int LAYOUT, int V = 0, int DS = 0>
 __global__ __launch_bounds__(kThreads) void pq_encode_cs_kernel(
-    const float* __restrict__ x, int64_t n, int d, int M, int dsub, int64_t rows_per_wg,
+    const float* __restrict__ x, int64_t n, int d, int M, int dsub_in, int64_t rows_per_wg,
     const float* __restrict__ C, const float* __restrict__ cn, const half8* __restrict__ img,
     const float* __restrict__ hinit, const float4* __restrict__ bnd, uint8_t* __restrict__ codesT,
     uint2* __restrict__ items, int2* __restrict__ counts) {
@@ -173,6 +175,7 @@ __global__ __launch_bounds__(kThreads) void pq_encode_cs_kernel(
     float* cnl = hb + 256;
     int* ctr = reinterpret_cast<int*>(cnl + 256);  // [0] pairs, [1] full, [2] resolve batches
 
+    const int dsub = DS > 0 ? DS : dsub_in;
     const int tid = threadIdx.x;
     const int w = __builtin_amdgcn_readfirstlane(tid >> 6), l = tid & 63;  // w: wave-uniform (SGPR)
     const int r = l & 31, h = l >> 5;
@@ -888,6 +891,9 @@ hipError_t launch_pq_encode_cs_v(const float* x, int64_t n, int d, int M, int ds
     const int layout = cs_layout(dsub);
     auto kern = layout == 1 ? pq_encode_cs_kernel<KS, 1, V>
               : layout == 3 ? pq_encode_cs_kernel<KS, 3, V> : pq_encode_cs_kernel<KS, 0, V>;
+    if constexpr (KS == 6) {
+        if (dsub == 96) kern = pq_encode_cs_kernel<6, 3, V, 96>;
+    }
     hipError_t e = hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, smem);
     if (e != hipSuccess) return e;
     constexpr int rsmem = resolve_smem_bytes<KS>();

@@ -63,12 +63,12 @@ __global__ __launch_bounds__(256) void rabitq_encode_kernel(const float* __restr
     orl2 = wave_sum(orl2);
     dp = wave_sum(dp);
     if (lane == 0) {
-        const float inv_d_sqrt = d == 0 ? 1.0f : __fdiv_rn(1.0f, __fsqrt_rn((float)d));
-        const float inv_norm = fabsf(l2) < FLT_EPSILON ? 1.0f : __fdiv_rn(1.0f, __fsqrt_rn(l2));
+        const float inv_d_sqrt = d == 0 ? 1.0f : __fdiv_rn(1.0f, sqrtf((float)d));
+        const float inv_norm = fabsf(l2) < FLT_EPSILON ? 1.0f : __fdiv_rn(1.0f, sqrtf(l2));
         const float ndp = __fmul_rn(__fmul_rn(dp, inv_norm), inv_d_sqrt);
         const float inv_dp = fabsf(ndp) < FLT_EPSILON ? 1.0f : __fdiv_rn(1.0f, ndp);
         const float f0 = metric == MIVQ_METRIC_INNER_PRODUCT ? __fsub_rn(l2, orl2) : l2;
-        const float f1 = __fmul_rn(inv_dp, __fsqrt_rn(l2));
+        const float f1 = __fmul_rn(inv_dp, sqrtf(l2));
         // the trailer is 4-byte aligned only when nb % 4 == 0: write bytes
         const uint32_t u0 = __float_as_uint(f0), u1 = __float_as_uint(f1);
 #pragma unroll
@@ -92,7 +92,7 @@ __global__ void rabitq_decode_kernel(const uint8_t* __restrict__ codes, int64_t 
 #pragma unroll
     for (int q = 0; q < 4; ++q) mu |= (uint32_t)code[nb + 4 + q] << (8 * q);
     const float mult = __uint_as_float(mu);
-    const float inv_d_sqrt = __fdiv_rn(1.0f, __fsqrt_rn((float)d));
+    const float inv_d_sqrt = __fdiv_rn(1.0f, sqrtf((float)d));
     const float bit = ((code[j >> 3] >> (j & 7)) & 1u) ? 1.0f : 0.0f;
     const float a = __fmul_rn(__fsub_rn(bit, 0.5f), mult);
     const float b = __fmul_rn(a, 2.0f);

@@ -5,6 +5,8 @@
 
 #include "mivq_common.h"
 
+#include <functional>
+
 namespace mivq {
 
 constexpr uint32_t kNoId = 0xFFFFFFFFu;
@@ -82,6 +84,11 @@ struct WaveTopK {
 hipError_t launch_topk_merge(const float* pd, const uint32_t* pi, int parts, int64_t nq, int k, float* od,
                              uint32_t* oi, hipStream_t st);
 
+// Tiled top-k (ivf.hip): a key-block producer + segmented top-k + running merge.  The
+// workspace of flat_tiled_workspace_bytes serves both launchers.
+using TileFn = std::function<hipError_t(int64_t c0, int64_t m, float* buf)>;
+hipError_t launch_tiled_topk(int64_t nq, int64_t n, int k, int64_t id_offset, void* ws, float* dists,
+                             uint32_t* ids, hipStream_t st, const TileFn& tile);
 // Tiled exact brute force (ivf.hip): pairwise chains + segmented top-k + running merge.
 size_t flat_tiled_workspace_bytes(int64_t nq, int64_t n, int k);
 hipError_t launch_flat_tiled(const float* q, int64_t nq, const float* x, int64_t n, int d, int metric, int k,

@@ -59,6 +59,9 @@ SIGNATURES = {
     "mivq_sq_decode_f64": (_c.c_int, [_vp, _i64, _i32, _vp, _vp, _i32, _vp, _vp]),
     "mivq_rabitq_encode": (_c.c_int, [_vp, _i64, _i32, _vp, _i32, _vp, _vp]),
     "mivq_rabitq_decode": (_c.c_int, [_vp, _i64, _i32, _vp, _vp, _vp]),
+    "mivq_rabitq_search_workspace_bytes": (_sz, [_i64, _i64, _i32, _i32]),
+    "mivq_rabitq_search": (_c.c_int, [_vp, _i64, _i32, _vp, _vp, _i64, _i32, _i32, _i32, _i64, _vp, _sz, _vp, _vp,
+                                      _vp]),
     "mivq_extrabitq_normalize": (_c.c_int, [_vp, _i32, _i64, _i32, _vp, _vp, _vp, _vp]),
     "mivq_extrabitq_quantize": (_c.c_int, [_vp, _i64, _i32, _vp, _i32, _vp, _vp, _vp]),
     "mivq_extrabitq_dequantize": (_c.c_int, [_vp, _i64, _i32, _vp, _i32, _vp, _vp]),
@@ -322,6 +325,25 @@ def rabitq_decode(codes: torch.Tensor, d: int, centroid: Optional[torch.Tensor])
     out = torch.empty((n, d), dtype=torch.float32, device=codes.device)
     _call("mivq_rabitq_decode", _ptr(codes), n, d, _ptr(centroid), _ptr(out), _stream())
     return out
+
+
+def rabitq_search(codes: torch.Tensor, d: int, centroid: Optional[torch.Tensor], q: torch.Tensor, qb: int,
+                  metric: int, k: int, id_offset: int = 0) -> Tuple[torch.Tensor, torch.Tensor]:
+    """IndexRaBitQ estimator search: (keys f32 (nq, k), ids int32 (nq, k) holding uint32 ids);
+    L2 keys are distance estimates, IP keys negated inner-product estimates (ascending)."""
+    _check(codes, "codes", torch.uint8, 2)
+    _check(q, "q", torch.float32, 2)
+    if centroid is not None:
+        _check(centroid, "centroid", torch.float32, 1)
+    if codes.shape[1] != rabitq_code_size(d) or q.shape[1] != d:
+        raise ValueError(f"codes rows {codes.shape[1]} B / queries d={q.shape[1]} do not match d={d}")
+    n, nq = codes.shape[0], q.shape[0]
+    dists = torch.empty((nq, k), dtype=torch.float32, device=q.device)
+    ids = torch.empty((nq, k), dtype=torch.int32, device=q.device)
+    ws = workspace(load_library().mivq_rabitq_search_workspace_bytes(nq, n, d, k), q.device)
+    _call("mivq_rabitq_search", _ptr(codes), n, d, _ptr(centroid), _ptr(q), nq, qb, metric, k, id_offset, _ptr(ws),
+          ws.numel(), _ptr(dists), _ptr(ids), _stream())
+    return dists, ids
 
 
 # ----------------------------------------------------------------- Extended RaBitQ

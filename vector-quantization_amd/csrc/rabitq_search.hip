@@ -28,6 +28,7 @@ namespace {
 
 typedef int v4i __attribute__((ext_vector_type(4)));
 typedef int v16i __attribute__((ext_vector_type(16)));
+typedef uint32_t u32x4a4 __attribute__((ext_vector_type(4), aligned(4)));  // code rows are 4-B aligned
 
 constexpr int kQfStride = 8;  // floats per query: c1, c2, c34, qc, qn, 1/sqrt(d), off, 0
 
@@ -117,24 +118,26 @@ __device__ __forceinline__ float load_f32(const unsigned char* p) {
     return __uint_as_float(u);
 }
 
-constexpr int kEstTiles = 8;  // 32-code tiles per wave (each workgroup: 4 waves x 256 codes)
+constexpr int kEstWaves = 8;  // waves per workgroup (all share the query block in LDS)
+constexpr int kEstTiles = 4;  // 32-code tiles per wave (each workgroup: 8 waves x 128 codes)
 
-// Grid (ceil(m / 1024), ceil(nq / 32)), 256 threads.  LDS: the 32 query rows (int8, pitch
-// d + 16), per wave one 32-code staging tile (32 x cs bytes) and the codes' popcounts.
-__global__ __launch_bounds__(256) void rabitq_est_mfma_kernel(const uint8_t* __restrict__ codes, int64_t m, int d,
-                                                              const int8_t* __restrict__ qq,
-                                                              const float* __restrict__ qf, int64_t nq, int metric,
-                                                              float* __restrict__ buf) {
+// Grid (ceil(m / (32 kEstWaves kEstTiles)), ceil(nq / 32)), 512 threads.  LDS holds only the
+// 32 query rows (int8, pitch d + 16), so two workgroups fit a CU up to d = 2048 and one up to
+// d = 4096.  Lane (r, h) of a wave owns code r of the tile and, per 32-dim k-step s, the 16
+// sign bits of dims 32s + 16h .. +16: the low (h = 0) or high half of the row's dword s, read
+// straight from memory four k-steps (one 16-B load) ahead of use.  Popcounts and the two
+// factors of code r move to the accumulator lanes by shuffles.
+__global__ __launch_bounds__(kEstWaves * 64) void rabitq_est_mfma_kernel(
+    const uint8_t* __restrict__ codes, int64_t m, int d, const int8_t* __restrict__ qq, const float* __restrict__ qf,
+    int64_t nq, int metric, float* __restrict__ buf) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     const int nb = d >> 3, cs = nb + 8;  // d % 32 == 0: cs % 4 == 0
     const int QP = d + 16;
     int8_t* qs = reinterpret_cast<int8_t*>(smem);
-    unsigned char* cst_all = smem + 32 * QP;
-    int* pop_all = reinterpret_cast<int*>(cst_all + 4 * 32 * cs);
     const int tid = threadIdx.x, w = tid >> 6, l = tid & 63, r = l & 31, h = l >> 5;
     const int64_t q0 = (int64_t)blockIdx.y * 32;
     const int qch = d >> 4;
-    for (int e = tid; e < 32 * qch; e += 256) {
+    for (int e = tid; e < 32 * qch; e += kEstWaves * 64) {
         const int row = e / qch, c = e - row * qch;
         uint4 v = make_uint4(0u, 0u, 0u, 0u);
         if (q0 + row < nq) v = *reinterpret_cast<const uint4*>(qq + (q0 + row) * d + 16 * c);
@@ -150,52 +153,55 @@ __global__ __launch_bounds__(256) void rabitq_est_mfma_kernel(const uint8_t* __r
         c1 = f[0]; c2 = f[1]; c34 = f[2]; qc = f[3]; qn = f[4]; off = (int)f[6];
     }
     const bool ip = metric == MIVQ_METRIC_INNER_PRODUCT;
-    unsigned char* cst = cst_all + w * 32 * cs;
-    int* pops = pop_all + w * 64;
-    const int nks = d >> 5;
-    const int ndw = 8 * cs;  // dwords per 32-code tile
+    const int nks = d >> 5;  // k-steps; nks % 4 handled by the dword tail
+    const int8_t* qrow = qs + r * QP + 16 * h;
+    const int sh = 16 * h;
     for (int t = 0; t < kEstTiles; ++t) {
-        const int64_t cb = ((int64_t)blockIdx.x * 4 * kEstTiles + w * kEstTiles + t) * 32;
-        if (cb >= m) break;
+        const int64_t cb = (((int64_t)blockIdx.x * kEstWaves + w) * kEstTiles + t) * 32;
+        if (cb >= m) break;  // wave-uniform
         const int nc = (int)min<int64_t>(32, m - cb);
-        const uint32_t* src = reinterpret_cast<const uint32_t*>(codes + cb * cs);
-        const int nvalid = nc * cs / 4;
-        for (int e = l; e < ndw; e += 64) reinterpret_cast<uint32_t*>(cst)[e] = e < nvalid ? src[e] : 0u;
-        lds_fence();
+        // rows past the chunk read row 0 of the tile (in range) and are never written
+        const uint8_t* crow = codes + (cb + (r < nc ? r : 0)) * cs;
         v16i acc = {};
         int pc = 0;
-        const unsigned char* crow = cst + r * cs + 2 * h;
-        for (int s = 0; s < nks; ++s) {
-            const uint32_t b16 = *reinterpret_cast<const uint16_t*>(crow + 4 * s);
+        auto kstep = [&](uint32_t dw, int s) __attribute__((always_inline)) {
+            const uint32_t b16 = (dw >> sh) & 0xFFFFu;
             pc += __builtin_popcount(b16);
             v4i av;
 #pragma unroll
             for (int j = 0; j < 4; ++j) av[j] = (int)(__umul24((b16 >> (4 * j)) & 0xFu, 0x204081u) & 0x01010101u);
-            const v4i bq = *reinterpret_cast<const v4i*>(qs + r * QP + 32 * s + 16 * h);
+            const v4i bq = *reinterpret_cast<const v4i*>(qrow + 32 * s);
             acc = __builtin_amdgcn_mfma_i32_32x32x32_i8(av, bq, acc, 0, 0, 0);
-        }
-        pops[2 * r + h] = pc;
-        lds_fence();
-        if (qok) {
-            float* orow = buf + qa * m + cb;
-#pragma unroll
-            for (int g = 0; g < 4; ++g) {
-#pragma unroll
-                for (int u = 0; u < 4; ++u) {
-                    const int ci = 8 * g + 4 * h + u;  // code row of accumulator 4g + u
-                    if (ci < nc) {
-                        const int pop = pops[2 * ci] + pops[2 * ci + 1];
-                        const int dot = acc[4 * g + u] + off * pop;
-                        const unsigned char* tr = cst + ci * cs + nb;
-                        const float f0 = *reinterpret_cast<const float*>(tr);
-                        const float f1 = *reinterpret_cast<const float*>(tr + 4);
-                        const float fd = __builtin_fmaf(c1, (float)dot, __builtin_fmaf(c2, (float)pop, -c34));
-                        orow[ci] = rabitq_key(fd, f0, f1, qc, qn, ip);
-                    }
-                }
+        };
+        const int n4 = nks >> 2;
+        if (n4 > 0) {
+            u32x4a4 cur = *reinterpret_cast<const u32x4a4*>(crow);  // cs % 4 == 0: 4-B aligned rows
+            for (int g = 0; g < n4; ++g) {
+                const u32x4a4 nxt = g + 1 < n4 ? *reinterpret_cast<const u32x4a4*>(crow + 16 * (g + 1)) : cur;
+                kstep(cur[0], 4 * g + 0);
+                kstep(cur[1], 4 * g + 1);
+                kstep(cur[2], 4 * g + 2);
+                kstep(cur[3], 4 * g + 3);
+                cur = nxt;
             }
         }
-        lds_fence();  // the next tile restages cst / pops
+        for (int s = 4 * n4; s < nks; ++s) kstep(*reinterpret_cast<const uint32_t*>(crow + 4 * s), s);
+        const float fr = *reinterpret_cast<const float*>(crow + nb + 4 * h);  // h = 0: f0, h = 1: f1 of code r
+        // every lane takes part in the shuffles (a bpermute from an inactive lane reads 0);
+        // only the stores are guarded
+        float* orow = buf + (qok ? qa : 0) * m + cb;
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                const int ci = 8 * g + 4 * h + u;  // code row of accumulator 4g + u
+                const int pop = __shfl(pc, ci) + __shfl(pc, ci + 32);
+                const float f0 = __shfl(fr, ci), f1 = __shfl(fr, ci + 32);
+                const int dot = acc[4 * g + u] + off * pop;
+                const float fd = __builtin_fmaf(c1, (float)dot, __builtin_fmaf(c2, (float)pop, -c34));
+                if (qok && ci < nc) orow[ci] = rabitq_key(fd, f0, f1, qc, qn, ip);
+            }
+        }
     }
 }
 
@@ -287,7 +293,7 @@ extern "C" int mivq_rabitq_search(const uint8_t* codes, int64_t n, int32_t d, co
         return e == hipSuccess ? MIVQ_OK : set_error(MIVQ_ERR_HIP, "rabitq_search: %s", hipGetErrorString(e));
     }
     const bool mfma = qb > 0 && (d % 32) == 0 && (reinterpret_cast<uintptr_t>(codes) % 4) == 0;
-    const size_t smem = (size_t)32 * (d + 16) + (size_t)4 * 32 * (d / 8 + 8) + 4 * 64 * sizeof(int);
+    const size_t smem = (size_t)32 * (d + 16);
     if (mfma && smem > 160 * 1024) return set_error(MIVQ_ERR_UNSUPPORTED, "rabitq_search: d=%d too large", d);
     if (mfma) {
         hipError_t e = hipFuncSetAttribute((const void*)rabitq_est_mfma_kernel,
@@ -299,9 +305,9 @@ extern "C" int mivq_rabitq_search(const uint8_t* codes, int64_t n, int32_t d, co
         nq, n, k, id_offset, p + L.tiled, dists, ids, st, [&](int64_t c0, int64_t m, float* buf) {
             const uint8_t* cc = codes + c0 * nbytes;
             if (mfma)
-                hipLaunchKernelGGL(rabitq_est_mfma_kernel, dim3((unsigned)ceil_div(m, 4 * kEstTiles * 32),
+                hipLaunchKernelGGL(rabitq_est_mfma_kernel, dim3((unsigned)ceil_div(m, kEstWaves * kEstTiles * 32),
                                                                 (unsigned)ceil_div(nq, 32)),
-                                   dim3(256), smem, st, cc, m, d, qq, qf, nq, metric, buf);
+                                   dim3(kEstWaves * 64), smem, st, cc, m, d, qq, qf, nq, metric, buf);
             else
                 hipLaunchKernelGGL(rabitq_est_generic_kernel, dim3((unsigned)ceil_div(m, 256), (unsigned)nq),
                                    dim3(256), 0, st, cc, m, d, qq, qr, qf, qb, metric, buf);

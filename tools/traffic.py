@@ -2,7 +2,7 @@
 
 usage: python tools/traffic.py gpurun_out/pmc_<tag> <workload> [last_n]
 Sums the per-launch HBM bytes (FETCH_SIZE x2 + WRITE_SIZE, gfx950 corrections as in
-tools/pmc_summary.py) of the three kernels of one encode call.
+tools/pmc_summary.py) of the four kernels of one encode call.
 """
 import csv
 import glob
@@ -11,7 +11,7 @@ import sys
 from collections import defaultdict
 from pathlib import Path
 
-KERNELS = ("pq_encode_cs_kernel", "pq_resolve_cs_kernel", "pq_transpose_codes_kernel")
+KERNELS = ("pq_encode_cs_kernel", "pq_resolve_full_kernel", "pq_resolve_cs_kernel", "pq_transpose_codes_kernel")
 
 
 def per_launch(root, sub, last_n):

@@ -66,6 +66,20 @@ __device__ __forceinline__ void top3_insert(float& t1, float& t2, float& t3, flo
     t1 = n1; t2 = n2; t3 = n3;
 }
 
+// Keeps the two largest: t1' = max(t1, v), t2' = med3(t1, t2, v) (same asm reasons).
+__device__ __forceinline__ void top2_insert(float& t1, float& t2, float v) {
+    float n1, n2;
+    asm("v_max_f32 %0, %1, %2" : "=v"(n1) : "v"(t1), "v"(v));
+    asm("v_med3_f32 %0, %1, %2, %3" : "=v"(n2) : "v"(t1), "v"(t2), "v"(v));
+    t1 = n1; t2 = n2;
+}
+
+__device__ __forceinline__ float fmax_raw(float a, float b) {
+    float o;
+    asm("v_max_f32 %0, %1, %2" : "=v"(o) : "v"(a), "v"(b));
+    return o;
+}
+
 // (v & 0xFFFFFF00) | k in ONE v_and_or_b32: gfx950's VOP3 takes no literal and one scalar
 // operand, so the mask must live in a VGPR (opaque_mask hides the constant from the
 // folder) and k comes from an SGPR.  Plain C, not inline asm: the compiler must see the
@@ -281,7 +295,19 @@ __global__ __launch_bounds__(kThreads) void pq_encode_cs_kernel(
         if (vb + kDepth * kWaves < nvb && !((V & 64) && vb >= kWaves)) load(vb + kDepth * kWaves, xr);
         xx += __shfl_xor(xx, 32);
 
+        // Candidates: the 16 packed scores of centroid block cb in this lane form a group; each
+        // group keeps its top-2 (g1, g2: pack + max + med3 per score), and (t1, t2, t3) is the
+        // top-3 of all groups' top-2s.  t1, t2 are then the lane's true first and second; a
+        // value that no group's top-2 holds lies below its group's g2, so with R = max g2:
+        //   t2 < thr                        -> one candidate,
+        //   t2 >= thr, t3 < thr, R < thr    -> exactly two (t1, t2),
+        //   t3 >= thr or R >= thr           -> possibly more: full item.
+        // R is folded into the third slot (t3 := max(t3, R) after each group): R <= t2 always,
+        // so the inserts keep t1, t2 exact and t3 = max(third, R), also across the lane-pair
+        // merge.  (A pair inside one group becomes a full item: about 1/16 of the pairs.)
+        // V&16384: the plain lane-wide top-3 (4 ops per score) instead.
         float t1 = -INFINITY, t2 = -INFINITY, t3 = -INFINITY;
+        constexpr bool kGroups = (V & 16384) == 0;
         constexpr int NCB = (V & 16) ? 0 : (V & 32) ? 1 : 8;
         // MFMAs of centroid block cb+1 go into the other accumulator before the top-3 of cb
         // reads this one, so a wave's matrix and vector work overlap
@@ -306,9 +332,20 @@ __global__ __launch_bounds__(kThreads) void pq_encode_cs_kernel(
             for (int cb = 0; cb < NCB; ++cb) {
                 floatx16 acc_next;
                 if (cb + 1 < NCB) acc_next = scores(cb + 1);
+                if constexpr (kGroups) {
+                    float g1 = -INFINITY, g2 = -INFINITY;
 #pragma unroll
-                for (int i = 0; i < 16; ++i)
-                    top3_insert(t1, t2, t3, pack_idx(acc_cur[i], vmask, (uint32_t)(cb * 32 + (i & 3) + 8 * (i >> 2))));
+                    for (int i = 0; i < 16; ++i)
+                        top2_insert(g1, g2, pack_idx(acc_cur[i], vmask, (uint32_t)(cb * 32 + (i & 3) + 8 * (i >> 2))));
+                    top3_insert(t1, t2, t3, g1);
+                    top3_insert(t1, t2, t3, g2);
+                    t3 = fmax_raw(t3, g2);
+                } else {
+#pragma unroll
+                    for (int i = 0; i < 16; ++i)
+                        top3_insert(t1, t2, t3,
+                                    pack_idx(acc_cur[i], vmask, (uint32_t)(cb * 32 + (i & 3) + 8 * (i >> 2))));
+                }
                 if (cb + 1 < NCB) acc_cur = acc_next;
             }
         }

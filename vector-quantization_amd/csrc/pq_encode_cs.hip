@@ -66,11 +66,13 @@ __device__ __forceinline__ void top3_insert(float& t1, float& t2, float& t3, flo
     t1 = n1; t2 = n2; t3 = n3;
 }
 
-// Keeps the two largest: t1' = max(t1, v), t2' = med3(t1, t2, v) (same asm reasons).
-__device__ __forceinline__ void top2_insert(float& t1, float& t2, float v) {
-    float n1, n2;
-    asm("v_max_f32 %0, %1, %2" : "=v"(n1) : "v"(t1), "v"(v));
-    asm("v_med3_f32 %0, %1, %2, %3" : "=v"(n2) : "v"(t1), "v"(t2), "v"(v));
+// Two values at once: the largest of {t1, t2, a, b} is max3(t1, a, b) and the second is
+// max(med3(t1, a, b), t2) (t2 <= t1 <= the top of {t1, a, b}): 3 ops for 2 values.
+__device__ __forceinline__ void top2_insert2(float& t1, float& t2, float a, float b) {
+    float n1, md, n2;
+    asm("v_max3_f32 %0, %1, %2, %3" : "=v"(n1) : "v"(t1), "v"(a), "v"(b));
+    asm("v_med3_f32 %0, %1, %2, %3" : "=v"(md) : "v"(t1), "v"(a), "v"(b));
+    asm("v_max_f32 %0, %1, %2" : "=v"(n2) : "v"(md), "v"(t2));
     t1 = n1; t2 = n2;
 }
 
@@ -296,7 +298,7 @@ __global__ __launch_bounds__(kThreads) void pq_encode_cs_kernel(
         xx += __shfl_xor(xx, 32);
 
         // Candidates: the 16 packed scores of centroid block cb in this lane form a group; each
-        // group keeps its top-2 (g1, g2: pack + max + med3 per score), and (t1, t2, t3) is the
+        // group keeps its top-2 (g1, g2: pack, then max3 + med3 + max per two scores), and (t1, t2, t3) is the
         // top-3 of all groups' top-2s.  t1, t2 are then the lane's true first and second; a
         // value that no group's top-2 holds lies below its group's g2, so with R = max g2:
         //   t2 < thr                        -> one candidate,
@@ -335,8 +337,11 @@ __global__ __launch_bounds__(kThreads) void pq_encode_cs_kernel(
                 if constexpr (kGroups) {
                     float g1 = -INFINITY, g2 = -INFINITY;
 #pragma unroll
-                    for (int i = 0; i < 16; ++i)
-                        top2_insert(g1, g2, pack_idx(acc_cur[i], vmask, (uint32_t)(cb * 32 + (i & 3) + 8 * (i >> 2))));
+                    for (int i = 0; i < 16; i += 2)
+                        top2_insert2(g1, g2,
+                                     pack_idx(acc_cur[i], vmask, (uint32_t)(cb * 32 + (i & 3) + 8 * (i >> 2))),
+                                     pack_idx(acc_cur[i + 1], vmask,
+                                              (uint32_t)(cb * 32 + ((i + 1) & 3) + 8 * ((i + 1) >> 2))));
                     top3_insert(t1, t2, t3, g1);
                     top3_insert(t1, t2, t3, g2);
                     t3 = fmax_raw(t3, g2);

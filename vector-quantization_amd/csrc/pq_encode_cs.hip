@@ -76,10 +76,18 @@ __device__ __forceinline__ void top2_insert2(float& t1, float& t2, float a, floa
     t1 = n1; t2 = n2;
 }
 
-__device__ __forceinline__ float fmax_raw(float a, float b) {
-    float o;
-    asm("v_max_f32 %0, %1, %2" : "=v"(o) : "v"(a), "v"(b));
-    return o;
+// Merges a group's sorted (g1 >= g2) into the lane state (t1 >= t2 >= t3, t3 holding
+// max(third, every group's second)): t1' = max(t1, g1), t2' = med3(t1, g1, max(t2, g2))
+// (second of the union), t3' = max3(t3, min(t2, g1), g2) (third of the union, min(t1, g2) <=
+// g2 folded into the g2 term).  5 ops.
+__device__ __forceinline__ void merge_group(float& t1, float& t2, float& t3, float g1, float g2) {
+    float a, b, n1, n2, n3;
+    asm("v_max_f32 %0, %1, %2" : "=v"(a) : "v"(t2), "v"(g2));
+    asm("v_min_f32 %0, %1, %2" : "=v"(b) : "v"(t2), "v"(g1));
+    asm("v_med3_f32 %0, %1, %2, %3" : "=v"(n2) : "v"(t1), "v"(g1), "v"(a));
+    asm("v_max_f32 %0, %1, %2" : "=v"(n1) : "v"(t1), "v"(g1));
+    asm("v_max3_f32 %0, %1, %2, %3" : "=v"(n3) : "v"(t3), "v"(b), "v"(g2));
+    t1 = n1; t2 = n2; t3 = n3;
 }
 
 // (v & 0xFFFFFF00) | k in ONE v_and_or_b32: gfx950's VOP3 takes no literal and one scalar
@@ -342,9 +350,7 @@ __global__ __launch_bounds__(kThreads) void pq_encode_cs_kernel(
                                      pack_idx(acc_cur[i], vmask, (uint32_t)(cb * 32 + (i & 3) + 8 * (i >> 2))),
                                      pack_idx(acc_cur[i + 1], vmask,
                                               (uint32_t)(cb * 32 + ((i + 1) & 3) + 8 * ((i + 1) >> 2))));
-                    top3_insert(t1, t2, t3, g1);
-                    top3_insert(t1, t2, t3, g2);
-                    t3 = fmax_raw(t3, g2);
+                    merge_group(t1, t2, t3, g1, g2);
                 } else {
 #pragma unroll
                     for (int i = 0; i < 16; ++i)

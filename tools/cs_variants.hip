@@ -5,14 +5,17 @@
 
 #define VARIANT(v)                                                                                     \
     case v:                                                                                           \
-        return (int)mivq::launch_pq_encode_cs_v<6, v>(x, n, d, M, dsub, C, cn, img, hinit, bnd, codesT, items, counts, (hipStream_t)st);
+        return (int)mivq::launch_pq_encode_cs_v<6, v>(x, n, d, M, dsub, C, cn, img, hinit, bnd, pd, bnd2, codesT, items, \
+                                                      counts, pinfo, (hipStream_t)st);
 
 extern "C" __attribute__((visibility("default"))) int cs_variant(int V, const float* x, int64_t n, int d, int M,
                                                                   int dsub, const float* C, const float* cn,
                                                                   const void* img, const float* hinit,
-                                                                  const void* bnd, uint8_t* codesT, void* items, void* counts, void* st) {
+                                                                  const void* bnd, const void* pd, const void* bnd2,
+                                                                  uint8_t* codesT, void* items, void* counts, void* pinfo,
+                                                                  void* st) {
     switch (V) {
-        VARIANT(0) VARIANT(1) VARIANT(2) VARIANT(4) VARIANT(8) VARIANT(17) VARIANT(33) VARIANT(65) VARIANT(145) VARIANT(256) VARIANT(513) VARIANT(1537) VARIANT(2561) VARIANT(4609) VARIANT(7681) VARIANT(16384)
+        VARIANT(0) VARIANT(1) VARIANT(2) VARIANT(4) VARIANT(8) VARIANT(17) VARIANT(33) VARIANT(65) VARIANT(145) VARIANT(256) VARIANT(513) VARIANT(1537) VARIANT(2561) VARIANT(4609) VARIANT(7681) VARIANT(16384) VARIANT(32768)
         default: return -1;
     }
 }

@@ -24,7 +24,7 @@ VARIANTS = {0: "encode + resolve", 1: "encode only", 2: "resolve: pairs only", 4
             17: "loads + convert + tile + fragments only", 65: "encode only, no x loads (compute alone)",
             145: "streaming only, subspace-major probe", 256: "encode + resolve, 256-wide full scans",
             513: "encode + full-item kernel", 1537: "... no exact chains", 2561: "... 1 of 8 filter blocks",
-            4609: "... no gathers", 7681: "... none of the three", 16384: "encode + resolve, lane-wide top-3 filter"}
+            4609: "... no gathers", 7681: "... none of the three", 16384: "encode + resolve, lane-wide top-3 filter", 32768: "encode + resolve, no pair window"}
 
 
 def prep_layout(M, dsub, ksub=256):
@@ -36,11 +36,16 @@ def prep_layout(M, dsub, ksub=256):
     L["ct"] = off; off = al(off + 4 * M * dsub * ksub)
     L["img"] = off; off = al(off + M * 8 * ks * 64 * 8 * 2)
     L["hinit"] = off; off = al(off + 4 * M * ksub)
-    L["bnd"] = off
+    L["bnd"] = off; off = al(off + 4 * M * 4)
+    L["spread"] = off; off = al(off + 4 * M * 2)
+    L["pd"] = off; off = al(off + (M * 256 * 256 * 8 if M <= 64 else 0))
+    L["bnd2"] = off
     return L
 
 
-def build():
+def build(lib=None):
+    if lib:
+        return ctypes.CDLL(str(ROOT / lib))
     so = ROOT / "tools" / "build" / "libcsvar.so"
     src = ROOT / "tools" / "cs_variants.hip"
     if not so.exists() or so.stat().st_mtime < max(src.stat().st_mtime, (ROOT / "vector-quantization_amd/csrc/pq_encode_cs.hip").stat().st_mtime):
@@ -58,8 +63,9 @@ def main():
     ap.add_argument("--reps", type=int, default=10)
     ap.add_argument("--data", default="clustered")
     ap.add_argument("--ab", default="", help="V1,V2: interleaved A/B timing instead of the variant table")
+    ap.add_argument("--lib", default="", help="prebuilt harness library (e.g. another MIVQ_CS_WAVES)")
     a = ap.parse_args()
-    lib = build()
+    lib = build(a.lib)
     dev = _native.require_device()
     X = synth(a.n, a.d, 0, dev, kind=a.data)
     probes(lib, X, a.reps)
@@ -72,14 +78,16 @@ def main():
     codesT = torch.empty((a.M, a.n), dtype=torch.uint8, device=dev)
     items = torch.empty((a.M * a.n * 8,), dtype=torch.uint8, device=dev)
     counts = torch.empty((a.M * a.n // 32 + 64, 2), dtype=torch.int32, device=dev)
+    pinfo = torch.empty((a.M * a.n * 8,), dtype=torch.uint8, device=dev)
     st = torch.cuda.current_stream().cuda_stream
     P = ctypes.c_void_p
 
     def run(v):
         rc = lib.cs_variant(ctypes.c_int(v), P(X.data_ptr()), ctypes.c_int64(a.n), ctypes.c_int(a.d), ctypes.c_int(a.M),
                             ctypes.c_int(dsub), P(C.data_ptr()), P(base + L["cn"]), P(base + L["img"]),
-                            P(base + L["hinit"]), P(base + L["bnd"]), P(codesT.data_ptr()),
-                            P(items.data_ptr()), P(counts.data_ptr()), P(st))
+                            P(base + L["hinit"]), P(base + L["bnd"]), P(base + L["pd"]), P(base + L["bnd2"]),
+                            P(codesT.data_ptr()), P(items.data_ptr()), P(counts.data_ptr()), P(pinfo.data_ptr()),
+                            P(st))
         assert rc == 0, rc
 
     if a.ab:

@@ -37,8 +37,13 @@ inline size_t align_up(size_t v, size_t a) { return (v + a - 1) / a * a; }
 //   hinit : (M, ksub)           f32  -||c||^2 / 2 * scale^2 (MFMA accumulator init)
 //   bnd   : (M, 4)              f32  per-subspace constants of the filter error bound
 //   spread: (M, 2)              u32  bits of Dmax, DDmax (pairwise spreads of the image)
+//   pd    : (M, 256, 256)       f32x2 per centroid pair {||c~_i - c~_j||, ||dc_i - dc_j||} (rounded
+//           up) for the pair window of the resolve kernel; only when M <= kPdMaxM
+//   bnd2  : (M, 4)              f32  {a_rest, b_rest, eta', 0}: the pair window's other terms
+constexpr int kPdMaxM = 64;  // pair-distance tables are kept for up to 64 subspaces (32 MiB)
+
 struct PqPrepLayout {
-    size_t cn, ct, img, hinit, bnd, spread, total;
+    size_t cn, ct, img, hinit, bnd, spread, pd, bnd2, total;
     int32_t dsub, ksub, ks;  // ks = padded dsub / 16 (k-steps of the f16 MFMA)
     bool mfma;               // filter path available for this shape
 };
@@ -56,6 +61,8 @@ inline PqPrepLayout pq_prep_layout(int32_t d, int32_t M, int32_t nbits) {
     L.hinit = off; off = align_up(off + sizeof(float) * (size_t)M * L.ksub, 256);
     L.bnd = off;   off = align_up(off + sizeof(float) * (size_t)M * 4, 256);
     L.spread = off; off = align_up(off + sizeof(uint32_t) * (size_t)M * 2, 256);
+    L.pd = off;     off = align_up(off + ((L.mfma && M <= kPdMaxM) ? (size_t)M * 256 * 256 * 8 : 0), 256);
+    L.bnd2 = off;   off = align_up(off + sizeof(float) * (size_t)M * 4, 256);
     L.total = off;
     return L;
 }

@@ -80,7 +80,7 @@ __device__ int subspace_scale_exp(const float* Cm, int dsub, float* red) {
 // squared sum <= (dsub + 3) 2^-24, covered by the (1 + 1e-5) applied to the norms); the
 // maxima of the squared sums go to spread[m] with atomicMax on their bits (non-negative).
 __global__ __launch_bounds__(256) void pq_prep_spread_kernel(const float* __restrict__ C, int dsub,
-                                                             uint32_t* __restrict__ spread) {
+                                                             uint32_t* __restrict__ spread, float2* __restrict__ pd) {
     __shared__ float red[256];
     const int m = blockIdx.x, g = blockIdx.y, tid = threadIdx.x;
     const float* Cm = C + (int64_t)m * 256 * dsub;
@@ -103,6 +103,9 @@ __global__ __launch_bounds__(256) void pq_prep_spread_kernel(const float* __rest
         // are skipped by fmaxf; inf gives inf -> the window is infinite
         d1 = fmaxf(d1, s1);
         d2 = fmaxf(d2, s2);
+        if (pd)  // the pair's own spreads (NaN stays NaN: the pair window then never settles it)
+            pd[((int64_t)m * 256 + i) * 256 + 16 * jj + (tid & 15)] =
+                make_float2(sqrtf(s1) * (1.0f + 1e-5f), sqrtf(s2) * (1.0f + 1e-5f));
     }
     atomicMax(&spread[2 * m + 0], __float_as_uint(d1));
     atomicMax(&spread[2 * m + 1], __float_as_uint(d2));
@@ -113,7 +116,7 @@ __global__ __launch_bounds__(256) void pq_prep_spread_kernel(const float* __rest
 __global__ void pq_prep_mfma_kernel(const float* __restrict__ C, const float* __restrict__ cn,
                                     int M, int dsub, int KS, half8* __restrict__ img,
                                     float* __restrict__ hinit, float4* __restrict__ bnd,
-                                    const uint32_t* __restrict__ spread) {
+                                    const uint32_t* __restrict__ spread, float4* __restrict__ bnd2) {
     const int m = blockIdx.x;
     const int tid = threadIdx.x;  // 256 threads
     __shared__ float red_nrm[256];
@@ -156,10 +159,15 @@ __global__ void pq_prep_mfma_kernel(const float* __restrict__ C, const float* __
         const float gd = (float)dsub * kU32 / (1.0f - (float)dsub * kU32);
         const float gn = (float)(dsub + 2) * kU32 / (1.0f - (float)(dsub + 2) * kU32);
         const float sq = sqrtf((float)dsub);
-        const float a = kUh * Dm + DDm + Cs * (2.004f * gn + 2.004f * kPack + 2.0f * (gd + kU32));
-        const float b = 1.001f * kEta * sq * Dm + Cs * Cs * (gn + 2.0f * gd + kPack + kU32);
+        const float a_rest = Cs * (2.004f * gn + 2.004f * kPack + 2.0f * (gd + kU32));
+        const float b_rest = Cs * Cs * (gn + 2.0f * gd + kPack + kU32);
+        const float eta1 = 1.001f * kEta * sq;
+        const float a = kUh * Dm + DDm + a_rest;
+        const float b = eta1 * Dm + b_rest;
         const bool ok = isfinite(Cs) && isfinite(a) && isfinite(b) && isfinite(Dm) && isfinite(DDm);
         bnd[m] = make_float4(sigma, ok ? a * 1.0625f : INFINITY, ok ? b * 1.0625f + 1e-30f : INFINITY, Cs);
+        // the pair window W12 = 1.0625 ((u_h Xs + eta') D_12 + Xs DD_12 + a_rest Xs + b_rest)
+        bnd2[m] = make_float4(ok ? a_rest : INFINITY, ok ? b_rest : INFINITY, eta1, 0.0f);
     }
 }
 
@@ -623,13 +631,14 @@ extern "C" int mivq_pq_prepare(const float* centroids, int32_t d, int32_t M, int
     if (L.mfma) {
         uint32_t* spread = reinterpret_cast<uint32_t*>(p + L.spread);
         if (hipMemsetAsync(spread, 0, sizeof(uint32_t) * 2 * (size_t)M, st) != hipSuccess) return check_launch("pq_prep_spread");
-        hipLaunchKernelGGL(pq_prep_spread_kernel, dim3(M, 16), dim3(256), 0, st, centroids, L.dsub, spread);
+        float2* pd = M <= kPdMaxM ? reinterpret_cast<float2*>(p + L.pd) : nullptr;
+        hipLaunchKernelGGL(pq_prep_spread_kernel, dim3(M, 16), dim3(256), 0, st, centroids, L.dsub, spread, pd);
         rc = check_launch("pq_prep_spread");
         if (rc) return rc;
         hipLaunchKernelGGL(pq_prep_mfma_kernel, dim3(M), dim3(256), 0, st, centroids,
                            reinterpret_cast<const float*>(p + L.cn), M, L.dsub, L.ks,
                            reinterpret_cast<half8*>(p + L.img), reinterpret_cast<float*>(p + L.hinit),
-                           reinterpret_cast<float4*>(p + L.bnd), spread);
+                           reinterpret_cast<float4*>(p + L.bnd), spread, reinterpret_cast<float4*>(p + L.bnd2));
         rc = check_launch("pq_prep_mfma");
     }
     return rc;
@@ -643,6 +652,7 @@ extern "C" size_t mivq_pq_encode_workspace_bytes(int64_t n, int32_t d, int32_t M
     // cs path: n*M uint2 resolve items; legacy MFMA path: its filter flags (never both)
     b += align_up(std::max((size_t)n * M * 8, (size_t)ceil_div(n, 32) * M * sizeof(uint32_t)), 256);
     b += align_up(cs_counts_bytes(n, M), 256);  // cs path: list counts per workgroup
+    b += align_up((size_t)n * M * 8, 256);      // cs path: per pair item {score gap, Xs}
     return b;
 }
 
@@ -674,6 +684,8 @@ extern "C" int mivq_pq_encode(const float* x, int64_t n, int32_t d, int32_t M, i
     void* items = ws + off;                                // cs path
     off += align_up(std::max((size_t)n * M * 8, (size_t)ceil_div(n, 32) * M * sizeof(uint32_t)), 256);
     void* counts = ws + off;
+    off += align_up(cs_counts_bytes(n, M), 256);
+    void* pinfo = ws + off;
 
     const bool aligned = (reinterpret_cast<uintptr_t>(x) % 16 == 0) && (d % 4 == 0) && (L.dsub % 4 == 0);
     const bool exact_only = (flags_in & MIVQ_PQ_FORCE_EXACT) != 0;
@@ -682,8 +694,9 @@ extern "C" int mivq_pq_encode(const float* x, int64_t n, int32_t d, int32_t M, i
     const bool mfma_ok = L.mfma && aligned && L.ks <= 8 && !exact_only && mfma_smem_bytes(L.ks, M) <= 160 * 1024;
     if (cs_ok) {
         const hipError_t e = launch_pq_encode_cs(L.ks, x, n, d, M, L.dsub, centroids, cn, p + L.img,
-                                                 reinterpret_cast<const float*>(p + L.hinit), p + L.bnd, codesT, items,
-                                                 counts, u8, st);
+                                                 reinterpret_cast<const float*>(p + L.hinit), p + L.bnd,
+                                                 M <= kPdMaxM ? p + L.pd : nullptr, p + L.bnd2, codesT, items,
+                                                 counts, pinfo, u8, st);
         if (e != hipSuccess) return set_error(MIVQ_ERR_HIP, "pq_encode_cs: %s", hipGetErrorString(e));
     } else if (mfma_ok) {
         const half8* img = reinterpret_cast<const half8*>(p + L.img);

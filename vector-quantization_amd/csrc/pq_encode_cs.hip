@@ -47,7 +47,10 @@ typedef float floatx16 __attribute__((ext_vector_type(16)));
 typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 
-constexpr int kWaves = 12;  // 768 threads, 3 waves per SIMD
+#ifndef MIVQ_CS_WAVES
+#define MIVQ_CS_WAVES 12
+#endif
+constexpr int kWaves = MIVQ_CS_WAVES;  // 768 threads, 3 waves per SIMD (profiling builds may override)
 constexpr int kDepth = 1;   // x blocks in flight per wave
 constexpr int kThreads = kWaves * 64;
 constexpr int kRsrcWord3 = 0x00020000;  // gfx9 buffer resource: 32-bit data format
@@ -188,7 +191,7 @@ __global__ __launch_bounds__(kThreads) void pq_encode_cs_kernel(
     const float* __restrict__ x, int64_t n, int d, int M, int dsub_in, int64_t rows_per_wg,
     const float* __restrict__ C, const float* __restrict__ cn, const half8* __restrict__ img,
     const float* __restrict__ hinit, const float4* __restrict__ bnd, uint8_t* __restrict__ codesT,
-    uint2* __restrict__ items, int2* __restrict__ counts) {
+    uint2* __restrict__ items, int2* __restrict__ counts, float2* __restrict__ pinfo) {
     constexpr int FR = 8 * KS * 64;
     constexpr int PITCH = 32 * KS + 16;  // bytes per fp16 tile row (16 B pad: conflict-free reads)
     constexpr int NIMAX = LAYOUT == 0 ? max_loads<KS>() : 2 * KS;
@@ -402,8 +405,12 @@ __global__ __launch_bounds__(kThreads) void pq_encode_cs_kernel(
             basef = __shfl(basef, 0);
             const uint64_t below = (1ull << l) - 1ull;
             uint2* list = items + (int64_t)m * n + r0;
-            if (mine && ncand == 2)
-                list[basep + __popcll(bp & below)] = make_uint2((uint32_t)rowl, (uint32_t)(k1 | (k2 << 8)));
+            if (mine && ncand == 2) {
+                // the pair kernel's own window needs the score gap (rounded down) and Xs
+                const int at = basep + __popcll(bp & below);
+                list[at] = make_uint2((uint32_t)rowl, (uint32_t)(k1 | (k2 << 8)));
+                pinfo[(int64_t)m * n + r0 + at] = make_float2(__fmul_rn(__fsub_rn(t1, t2), 0.99999988f), Xs);  // gap rounded down
+            }
             if (mine && ncand >= 3) list[nrows - 1 - (basef + __popcll(bfull & below))] = make_uint2((uint32_t)rowl, 0u);
         }
     };
@@ -433,14 +440,15 @@ constexpr int kRWaves = 8;
 
 template <int KS>
 constexpr int resolve_smem_bytes() {
-    return 128 * (2 * 16 * KS + 4) * 4 + 256 * 4 + kRWaves * 16 * (16 * KS + 4) * 4 + 16;
+    return 128 * (2 * 16 * KS + 4) * 4 + 256 * 4 + kRWaves * 16 * (16 * KS + 4) * 4 + 16 + kRWaves * 64 * 8;
 }
 
 template <int KS, int V = 0>
 __global__ __launch_bounds__(kRWaves * 64) void pq_resolve_cs_kernel(
     const float* __restrict__ x, int64_t n, int d, int M, int dsub, int64_t rows_per_wg,
     const float* __restrict__ C, const float* __restrict__ cn, uint8_t* __restrict__ codesT,
-    const uint2* __restrict__ items, const int2* __restrict__ counts, int with_full) {
+    const uint2* __restrict__ items, const int2* __restrict__ counts, int with_full, const float2* __restrict__ pd,
+    const float4* __restrict__ bnd2, const float2* __restrict__ pinfo) {
     constexpr int DP = 16 * KS;
     constexpr int PP = 2 * DP + 4;  // floats per centroid-pair row
     constexpr int SP = DP + 4;      // floats per staged x row
@@ -450,6 +458,7 @@ __global__ __launch_bounds__(kRWaves * 64) void pq_resolve_cs_kernel(
     float* cnl = cp + 128 * PP;
     float* stg_all = cnl + 256;
     int* ctr = reinterpret_cast<int*>(stg_all + kRWaves * 16 * SP);
+    uint2* comp_all = reinterpret_cast<uint2*>(ctr + 4);  // per wave: 64 compacted pair items
 
     const int tid = threadIdx.x;
     const int w = tid >> 6, l = tid & 63;
@@ -606,10 +615,36 @@ __global__ __launch_bounds__(kRWaves * 64) void pq_resolve_cs_kernel(
         } else {
             // ---- 64 pairs, one per lane: the canonical chains of its two candidates
             const int first = (b - nbf) * 64;
-            const int cntb = min(64, np - first);
-            const bool live = l < cntb;
+            const int cnt0 = min(64, np - first);
             uint2 it = make_uint2(0u, 0u);
-            if (live) it = list[first + l];
+            bool keep = l < cnt0;
+            if (keep) it = list[first + l];
+            if (pd != nullptr && keep) {
+                // The pair's own window: the f16 rounding of the score difference of k1 and k2
+                // is bounded with ||c~_k1 - c~_k2|| and ||dc_k1 - dc_k2|| instead of the
+                // subspace maxima (the other terms as in the filter window).  If t1 - t2 exceeds
+                // it, k2 cannot be the canonical winner: k1 is the code, no chains needed.
+                const float2 gi = pinfo[(int64_t)m * n + r0 + first + l];
+                const int q1 = (int)(it.y & 0xFFu), q2 = (int)((it.y >> 8) & 0xFFu);
+                const float2 dd = pd[((int64_t)m * 256 + q1) * 256 + q2];
+                const float4 b2 = bnd2[m];
+                const float w12 = 1.0625f * (fmaf(4.8828125e-4f, gi.y, b2.z) * dd.x + gi.y * dd.y +
+                                             b2.x * gi.y + b2.y);
+                if (gi.x > w12) {
+                    codesT[(int64_t)m * n + r0 + it.x] = (uint8_t)q1;
+                    keep = false;
+                }
+            }
+            // compact the remaining items into lanes 0 .. cntb-1
+            const uint64_t km = __ballot(keep);
+            const int cntb = __popcll(km);
+            uint2* comp = comp_all + w * 64;
+            if (keep) comp[__popcll(km & ((1ull << l) - 1ull))] = it;
+            lds_fence();
+            const bool live = l < cntb;
+            it = live ? comp[l] : make_uint2(0u, 0u);
+            lds_fence();
+            if (cntb == 0) continue;
             const int rowl = (int)it.x;
             float4 xv[NX];
 #pragma unroll
@@ -933,8 +968,8 @@ int cs_layout(int dsub) {
 
 template <int KS, int V>
 hipError_t launch_pq_encode_cs_v(const float* x, int64_t n, int d, int M, int dsub, const float* C, const float* cn,
-                                 const void* img, const float* hinit, const void* bnd, uint8_t* codesT, void* items,
-                                 void* counts, hipStream_t st) {
+                                 const void* img, const float* hinit, const void* bnd, const void* pd, const void* bnd2,
+                                 uint8_t* codesT, void* items, void* counts, void* pinfo, hipStream_t st) {
     const int smem = cs_smem_bytes(KS, dsub);
     const int layout = cs_layout(dsub);
     auto kern = layout == 1 ? pq_encode_cs_kernel<KS, 1, V>
@@ -955,7 +990,7 @@ hipError_t launch_pq_encode_cs_v(const float* x, int64_t n, int d, int M, int ds
     const int64_t grid = ceil_div(n, R) * M;
     hipLaunchKernelGGL(kern, dim3((unsigned)grid), dim3(kThreads), smem, st, x, n, d, M, dsub, R, C, cn,
                        static_cast<const half8*>(img), hinit, static_cast<const float4*>(bnd), codesT,
-                       static_cast<uint2*>(items), static_cast<int2*>(counts));
+                       static_cast<uint2*>(items), static_cast<int2*>(counts), static_cast<float2*>(pinfo));
     e = hipGetLastError();
     if (e != hipSuccess || ((V & 1) && !(V & 512))) return e;
     // full items through pq_resolve_full_kernel (filter re-run + candidate chains): 1.5-2 %
@@ -974,19 +1009,25 @@ hipError_t launch_pq_encode_cs_v(const float* x, int64_t n, int d, int M, int ds
         if (e != hipSuccess || (V & 1)) return e;  // V&513: the instrumented full kernel alone
     }
     hipLaunchKernelGGL(rkern, dim3((unsigned)grid), dim3(kRWaves * 64), rsmem, st, x, n, d, M, dsub, R, C, cn, codesT,
-                       static_cast<const uint2*>(items), static_cast<const int2*>(counts), mfma_full ? 0 : 1);
+                       static_cast<const uint2*>(items), static_cast<const int2*>(counts), mfma_full ? 0 : 1,
+                       (V & 32768) ? nullptr : static_cast<const float2*>(pd), static_cast<const float4*>(bnd2),
+                       static_cast<const float2*>(pinfo));
     return hipGetLastError();
 }
 
 size_t cs_counts_bytes(int64_t n, int M) { return (size_t)ceil_div(n, 32 * kWaves) * M * sizeof(int2); }
 
 hipError_t launch_pq_encode_cs(int KS, const float* x, int64_t n, int d, int M, int dsub, const float* C,
-                               const float* cn, const void* img, const float* hinit, const void* bnd,
-                               uint8_t* codesT, void* items, void* counts, uint8_t* codes, hipStream_t st) {
+                               const float* cn, const void* img, const float* hinit, const void* bnd, const void* pd,
+                               const void* bnd2, uint8_t* codesT, void* items, void* counts, void* pinfo,
+                               uint8_t* codes, hipStream_t st) {
     hipError_t e = hipErrorInvalidValue;
     switch (KS) {
 #define MIVQ_CS_CASE(k)                                                                                        \
-    case k: e = launch_pq_encode_cs_v<k, 0>(x, n, d, M, dsub, C, cn, img, hinit, bnd, codesT, items, counts, st); break;
+    case k:                                                                                                    \
+        e = launch_pq_encode_cs_v<k, 0>(x, n, d, M, dsub, C, cn, img, hinit, bnd, pd, bnd2, codesT, items, counts, \
+                                        pinfo, st);                                                            \
+        break;
         MIVQ_CS_CASE(1) MIVQ_CS_CASE(2) MIVQ_CS_CASE(3) MIVQ_CS_CASE(4) MIVQ_CS_CASE(5) MIVQ_CS_CASE(6)
 #undef MIVQ_CS_CASE
         default: return hipErrorInvalidValue;

@@ -913,6 +913,208 @@ __global__ __launch_bounds__(kFWaves * 64) void pq_resolve_full_kernel(
     }
 }
 
+// Full items, high-occupancy form (the library default; V&65536 selects the kernel above):
+// the same filter re-run and candidate chains, but without the fp32 codebook in LDS, so two
+// workgroups of 4 waves fit a CU.  The f16 A operands come straight from the prepared image
+// (fragment order, one 16-B load per lane, L2-resident), the scores are computed twice (a
+// max pass for the window, then a pass that collects the candidates: MFMAs are cheap here),
+// and the canonical chains read the centroid rows from memory.  Grid: kF2Slices workgroups
+// per encode workgroup's list; wave w of slice s takes batches s*4 + w, s*4 + w + 4*kF2Slices, ...
+constexpr int kF2Slices = 2;
+
+template <int KS>
+constexpr int full2_smem_bytes() {
+    return 256 * 4 + kFWaves * (32 * (16 * KS + 4) * 4 + 32 * kFCap * 4 + 32 * 4);
+}
+
+template <int KS, int DS>
+__global__ __launch_bounds__(kFWaves * 64) __attribute__((amdgpu_waves_per_eu(2))) void pq_resolve_full2_kernel(
+    const float* __restrict__ x, int64_t n, int d, int M, int dsub_in, int64_t rows_per_wg, unsigned enc_grid,
+    const float* __restrict__ C, const float* __restrict__ cn, const half8* __restrict__ img,
+    const float* __restrict__ hinit, const float4* __restrict__ bnd, uint8_t* __restrict__ codesT,
+    const uint2* __restrict__ items, const int2* __restrict__ counts) {
+    constexpr int DP = 16 * KS;  // padded dsub
+    constexpr int XP = DP + 4;   // floats per staged x row
+    constexpr int NL = 2 * KS;   // 16-B loads per lane per batch (32 rows of <= DP floats)
+    constexpr int FR = 8 * KS * 64;
+    const int dsub = DS > 0 ? DS : dsub_in;
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    float* hb = reinterpret_cast<float*>(smem);
+    const int tid = threadIdx.x;
+    const int w = __builtin_amdgcn_readfirstlane(tid >> 6), l = tid & 63;
+    const int r = l & 31, h = l >> 5;
+    float* xf = reinterpret_cast<float*>(smem + 256 * 4 + w * (32 * XP * 4 + 32 * kFCap * 4 + 32 * 4));
+    int* cand = reinterpret_cast<int*>(xf + 32 * XP);
+    int* ccnt = cand + 32 * kFCap;
+
+    const unsigned b = blockIdx.x / kF2Slices, sl = blockIdx.x % kF2Slices;
+    int m;
+    int64_t chunk;
+    wg_coords_of(b, enc_grid, M, m, chunk);
+    const int64_t r0 = chunk * rows_per_wg;
+    const int64_t r1 = min(n, r0 + rows_per_wg);
+    if (r0 >= r1) return;
+    const int nrows = (int)(r1 - r0);
+    const int nf = counts[b].y;
+    if (nf == 0) return;
+    hb[tid] = hinit[(int64_t)m * 256 + tid];
+    __syncthreads();
+
+    const float4 bm = bnd[m];
+    const float2v sig2 = {bm.x, bm.x};
+    const float xs_eta = 6.1035156e-5f * sqrtf((float)dsub);
+    const float* cnm = cn + (int64_t)m * 256;
+    const float* Cm = C + (int64_t)m * 256 * dsub;
+    const half8* im = img + (int64_t)m * FR;
+    const int q = dsub >> 2;
+    const int nld = (32 * q + 63) >> 6;
+    const uint2* list = items + (int64_t)m * n + r0;
+    const float* xsub = x + r0 * d + (int64_t)m * dsub;
+    const int nbat = (nf + 31) >> 5;
+
+    auto frag = [&](const float* src) __attribute__((always_inline)) {
+        const f32x4 a0 = *reinterpret_cast<const f32x4*>(src);
+        const f32x4 a1 = *reinterpret_cast<const f32x4*>(src + 4);
+        const float2v p0 = (float2v){a0.x, a0.y} * sig2, p1 = (float2v){a0.z, a0.w} * sig2;
+        const float2v p2 = (float2v){a1.x, a1.y} * sig2, p3 = (float2v){a1.z, a1.w} * sig2;
+        return (u32x4){cvt2(p0.x, p0.y), cvt2(p1.x, p1.y), cvt2(p2.x, p2.y), cvt2(p3.x, p3.y)};
+    };
+
+    for (int bt = (int)sl * kFWaves + w; bt < nbat; bt += kF2Slices * kFWaves) {
+        const int first = bt * 32;
+        const int cntb = min(32, nf - first);
+        int rowl = 0;
+        if (l < cntb) rowl = (int)list[nrows - 1 - (first + l)].x;
+        f32x4 v[NL];
+#pragma unroll
+        for (int j = 0; j < NL; ++j) {
+            const int c = j * 64 + l;
+            const int row = c / q, col = c - row * q;
+            const int src = __shfl(rowl, min(row, 31));
+            const bool ok = j < nld && row < cntb;
+            v[j] = *reinterpret_cast<const f32x4*>(xsub + (ok ? (int64_t)src * d + 4 * col : 0));
+        }
+#pragma unroll
+        for (int j = 0; j < NL; ++j) {
+            const int c = j * 64 + l;
+            const int row = c / q, col = c - row * q;
+            if (j < nld && row < 32) *reinterpret_cast<f32x4*>(xf + row * XP + 4 * col) = v[j];
+        }
+        if (DS == 0 || DS != DP)
+            for (int e = l; e < 32 * (DP - dsub); e += 64) {
+                const int row = e / (DP - dsub);
+                xf[row * XP + dsub + (e - row * (DP - dsub))] = 0.0f;
+            }
+        if (l < 32) ccnt[l] = 0;
+        lds_fence();
+        half8 bf[KS];
+        float xx = 0.0f;
+#pragma unroll
+        for (int ks = 0; ks < KS; ++ks) {
+            const u32x4 u = frag(xf + r * XP + h * 8 * KS + 8 * ks);
+            bf[ks] = __builtin_bit_cast(half8, u);
+            xx = dot2_self(u[0], xx); xx = dot2_self(u[1], xx);
+            xx = dot2_self(u[2], xx); xx = dot2_self(u[3], xx);
+        }
+        xx += __shfl_xor(xx, 32);
+        // an opaque zero tied to the batch keeps the image loads inside the loop (hoisted, the
+        // 8 * KS fragments would need 4 * 8 * KS registers)
+        const int oz = __builtin_amdgcn_readfirstlane(bt) >> 30;
+        const half8* imb = im + oz;
+        const float* hbb = hb + oz;  // (same for the accumulator init: 128 values per lane)
+        auto scores = [&](int cb) __attribute__((always_inline)) {
+            half8 a[KS];
+#pragma unroll
+            for (int ks = 0; ks < KS; ++ks) a[ks] = imb[(cb * KS + ks) * 64 + l];
+            floatx16 acc;
+#pragma unroll
+            for (int qq = 0; qq < 4; ++qq) {
+                const float4 hv = *reinterpret_cast<const float4*>(hbb + cb * 32 + 8 * qq + 4 * h);
+                acc[4 * qq + 0] = hv.x; acc[4 * qq + 1] = hv.y;
+                acc[4 * qq + 2] = hv.z; acc[4 * qq + 3] = hv.w;
+            }
+#pragma unroll
+            for (int ks = 0; ks < KS; ++ks) acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(a[ks], bf[ks], acc, 0, 0, 0);
+            return acc;
+        };
+        float t1 = -INFINITY;
+#pragma unroll 1
+        for (int cb = 0; cb < 8; ++cb) {
+            const floatx16 acc = scores(cb);
+#pragma unroll
+            for (int i = 0; i < 16; ++i) t1 = fmaxf(t1, acc[i]);
+        }
+        t1 = fmaxf(t1, __shfl_xor(t1, 32));
+        const float Xs = (sqrtf(xx) * (1.0f + 1e-5f) + xs_eta) * (1.0f + 9.765625e-4f);
+        const float W = bm.y * Xs + bm.z;
+        const float thr = t1 - W;
+        const bool bad = !(Xs < 65000.0f) || !isfinite(t1) || !isfinite(W);
+#pragma unroll 1
+        for (int cb = 0; cb < 8; ++cb) {
+            const floatx16 acc = scores(cb);
+#pragma unroll
+            for (int i = 0; i < 16; ++i) {
+                if (!bad && acc[i] >= thr) {
+                    const int slot = atomicAdd(&ccnt[r], 1);
+                    if (slot < kFCap) cand[r * kFCap + slot] = cb * 32 + (i & 3) + 8 * (i >> 2) + 4 * h;
+                }
+            }
+        }
+        lds_fence();
+        float bs = INFINITY;
+        int bk = 256;
+        const float* xr = xf + r * XP;
+        auto exact = [&](int k) __attribute__((always_inline)) {
+            const float* c = Cm + (int64_t)k * dsub;
+            float dot = 0.0f;
+            if constexpr (DS > 0 && DS % 8 == 0) {
+                // centroid row from memory, half a row in flight at a time; the x row is read
+                // from LDS per candidate (an opaque zero keeps those reads from being hoisted
+                // out of the candidate loop, where they would need 4 * DS / 4 registers)
+                const float* xk = xr + (__builtin_amdgcn_readfirstlane(k) >> 30);
+#pragma unroll
+                for (int hf = 0; hf < 2; ++hf) {
+                    f32x4 cv[DS / 8];
+#pragma unroll
+                    for (int t = 0; t < DS / 8; ++t) cv[t] = *reinterpret_cast<const f32x4*>(c + hf * (DS / 2) + 4 * t);
+#pragma unroll
+                    for (int t = 0; t < DS / 8; ++t) {
+                        const f32x4 xv = *reinterpret_cast<const f32x4*>(xk + hf * (DS / 2) + 4 * t);
+                        dot = __builtin_fmaf(xv.x, cv[t].x, dot);
+                        dot = __builtin_fmaf(xv.y, cv[t].y, dot);
+                        dot = __builtin_fmaf(xv.z, cv[t].z, dot);
+                        dot = __builtin_fmaf(xv.w, cv[t].w, dot);
+                    }
+                }
+            } else {
+                for (int t = 0; t < dsub; t += 4) {
+                    const f32x4 cv = *reinterpret_cast<const f32x4*>(c + t);
+                    const f32x4 xv = *reinterpret_cast<const f32x4*>(xr + t);
+                    dot = __builtin_fmaf(xv.x, cv.x, dot);
+                    dot = __builtin_fmaf(xv.y, cv.y, dot);
+                    dot = __builtin_fmaf(xv.z, cv.z, dot);
+                    dot = __builtin_fmaf(xv.w, cv.w, dot);
+                }
+            }
+            const float sc = __builtin_fmaf(-2.0f, dot, cnm[k]);
+            if (sc < bs || (sc == bs && k < bk)) { bs = sc; bk = k; }
+        };
+        if (r < cntb) {
+            const int nc = ccnt[r];
+            if (bad || nc > kFCap) {
+                for (int k = h; k < 256; k += 2) exact(k);
+            } else {
+                for (int j = h; j < nc; j += 2) exact(cand[r * kFCap + j]);
+            }
+        }
+        const float os = __shfl_xor(bs, 32);
+        const int ok = __shfl_xor(bk, 32);
+        if (os < bs || (os == bs && ok < bk)) { bs = os; bk = ok; }
+        if (h == 0 && r < cntb) codesT[(int64_t)m * n + r0 + rowl] = (uint8_t)((bs < INFINITY) ? bk : 0);
+        lds_fence();
+    }
+}
+
 // (M, n) -> (n, M): one block per 256 rows, the tile goes through LDS.
 __global__ __launch_bounds__(256) void pq_transpose_codes_kernel(const uint8_t* __restrict__ codesT, int64_t n, int M,
                                                                  uint8_t* __restrict__ codes) {
@@ -997,7 +1199,19 @@ hipError_t launch_pq_encode_cs_v(const float* x, int64_t n, int d, int M, int ds
     // faster end to end than the pair kernel's 256-wide scans (interleaved A/B, 1M x 1536);
     // V&256 restores the scans
     constexpr bool mfma_full = (V & 256) == 0;
-    if (mfma_full) {
+    if (mfma_full && !(V & 65536) && !(V & 512)) {
+        constexpr int fsmem = full2_smem_bytes<KS>();
+        auto fkern = (KS == 6 && dsub == 96) ? pq_resolve_full2_kernel<KS, (KS == 6 ? 96 : 0)>
+                                             : pq_resolve_full2_kernel<KS, 0>;
+        e = hipFuncSetAttribute((const void*)fkern, hipFuncAttributeMaxDynamicSharedMemorySize, fsmem);
+        if (e != hipSuccess) return e;
+        hipLaunchKernelGGL(fkern, dim3((unsigned)(grid * kF2Slices)), dim3(kFWaves * 64), fsmem, st, x, n, d, M, dsub,
+                           R, (unsigned)grid, C, cn, static_cast<const half8*>(img), hinit,
+                           static_cast<const float4*>(bnd), codesT, static_cast<const uint2*>(items),
+                           static_cast<const int2*>(counts));
+        e = hipGetLastError();
+        if (e != hipSuccess || (V & 1)) return e;
+    } else if (mfma_full) {
         constexpr int fsmem = full_smem_bytes<KS>();
         auto fkern = pq_resolve_full_kernel<KS, V>;
         e = hipFuncSetAttribute((const void*)fkern, hipFuncAttributeMaxDynamicSharedMemorySize, fsmem);

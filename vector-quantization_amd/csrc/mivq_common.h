@@ -35,7 +35,7 @@ inline size_t align_up(size_t v, size_t a) { return (v + a - 1) / a * a; }
 //   img   : (M, 8 cb, KS, 64 lanes, 8 halves) f16 MFMA A-operand image (ksub == 256,
 //           dsub padded to KS*16), see pq_encode.hip
 //   hinit : (M, ksub)           f32  -||c||^2 / 2 * scale^2 (MFMA accumulator init)
-//   bnd   : (M, 4)              f32  per-subspace constants of the filter error bound
+//   bnd   : (M, 4)              f32  {sigma, a, b, tau}: scales and the filter window W = a Xs + b
 //   spread: (M, 2)              u32  bits of Dmax, DDmax (pairwise spreads of the image)
 //   pd    : (M, 256, 256)       f32x2 per centroid pair {||c~_i - c~_j||, ||dc_i - dc_j||} (rounded
 //           up) for the pair window of the resolve kernel; only when M <= kPdMaxM

@@ -49,13 +49,16 @@ __global__ void pq_prep_norms_kernel(const float* __restrict__ C, int M, int ksu
 // Unit roundoffs used by the filter error bound.
 constexpr float kU32 = 5.9604645e-8f;    // 2^-24
 constexpr float kUh = 4.8828125e-4f;     // 2^-11: f32 -> f16 round-to-nearest-even
-constexpr float kEta = 6.1035156e-5f;    // 2^-14: |error| of an f16 denormal / flushed input
+// |error| of an f16 subnormal result: <= 2^-25 (round to nearest; the kernels are built with
+// f16 denormals preserved, .amdhsa_float_denorm_mode_16_64 = 3), taken as 2^-24.
+constexpr float kEta = 5.9604645e-8f;    // 2^-24
 constexpr float kPack = 3.0517578e-5f;   // 2^-15: 8 low mantissa bits replaced by the index
 constexpr int kScaleC = 14;              // max |c~| <= 2^14
 constexpr int kScaleX = 12;              // |x~| < 65504 while |x| < 2^4 * 2^ceil(log2 max|c|)
 
 // Scale exponent of subspace m: e = ceil(log2 max|c|) (clamped), tau = 2^(kScaleC - e),
-// sigma = 2^(kScaleX - e).  Block-wide (256 threads); `red` is 256 floats of LDS.
+// sigma = 2^(kScaleX - e) (or 1, see pq_prep_mfma_kernel).  Block-wide (256 threads); `red` is
+// 256 floats of LDS.
 __device__ int subspace_scale_exp(const float* Cm, int dsub, float* red) {
     const int tid = threadIdx.x;
     float mabs = 0.0f;
@@ -131,7 +134,10 @@ __global__ void pq_prep_mfma_kernel(const float* __restrict__ C, const float* __
     }
     const float cn_max = red_nrm[0];
     const float tau = ldexpf(1.0f, kScaleC - e);  // c~ = f16(tau * c)
-    const float sigma = ldexpf(1.0f, kScaleX - e);  // x~ = f16(sigma * x)
+    // x~ = f16(sigma * x).  sigma = 1 (no scaling multiply in the encode kernels) whenever the
+    // codebook's magnitude is ordinary; otherwise the power of two that puts sigma x in the f16
+    // range next to c~.  f16 subnormals of x~ cost at most 2^-25 each (kEta).
+    const float sigma = (e >= -8 && e <= 8) ? 1.0f : ldexpf(1.0f, kScaleX - e);
     const float st = sigma * tau;
     // operand image: fragment (cb, ks), lane l holds c~[cb*32 + (l&31)][t(ks, l>>5, j)]
     //   t(ks, h, j) = h*8*KS + 8*ks + j   (zero when t >= dsub)
@@ -152,20 +158,24 @@ __global__ void pq_prep_mfma_kernel(const float* __restrict__ C, const float* __
     // accumulator init: -(cn/2) * sigma * tau  (exact: powers of two)
     hinit[(int64_t)m * 256 + tid] = -0.5f * cn[(int64_t)m * 256 + tid] * st;
     if (tid == 0) {
-        // Window W(Xs) = a * Xs + b in accumulator units; Xs = sigma * ||x_m||, Cs = tau * Cmax.
+        // Window W(Xs) = a * Xs + b in accumulator units; Xs = sigma * ||x_m||, Cs = tau * Cmax,
+        // Hs = sigma * tau * Cmax^2 >= 2 |accumulator init| (the terms that scale with ||c||^2:
+        // rounding of cn and of the accumulation of the init, the canonical cn chain, the packed
+        // index bits).
         const float Cs = tau * sqrtf(cn_max) * (1.0f + 1e-6f);
+        const float Hs = st * cn_max * (1.0f + 1e-6f);
         const float Dm = sqrtf(__uint_as_float(spread[2 * m + 0])) * (1.0f + 1e-5f);
         const float DDm = sqrtf(__uint_as_float(spread[2 * m + 1])) * (1.0f + 1e-5f);
         const float gd = (float)dsub * kU32 / (1.0f - (float)dsub * kU32);
         const float gn = (float)(dsub + 2) * kU32 / (1.0f - (float)(dsub + 2) * kU32);
         const float sq = sqrtf((float)dsub);
         const float a_rest = Cs * (2.004f * gn + 2.004f * kPack + 2.0f * (gd + kU32));
-        const float b_rest = Cs * Cs * (gn + 2.0f * gd + kPack + kU32);
+        const float b_rest = Hs * (gn + 2.0f * gd + kPack + kU32);
         const float eta1 = 1.001f * kEta * sq;
         const float a = kUh * Dm + DDm + a_rest;
         const float b = eta1 * Dm + b_rest;
-        const bool ok = isfinite(Cs) && isfinite(a) && isfinite(b) && isfinite(Dm) && isfinite(DDm);
-        bnd[m] = make_float4(sigma, ok ? a * 1.0625f : INFINITY, ok ? b * 1.0625f + 1e-30f : INFINITY, Cs);
+        const bool ok = isfinite(Cs) && isfinite(Hs) && isfinite(a) && isfinite(b) && isfinite(Dm) && isfinite(DDm);
+        bnd[m] = make_float4(sigma, ok ? a * 1.0625f : INFINITY, ok ? b * 1.0625f + 1e-30f : INFINITY, tau);
         // the pair window W12 = 1.0625 ((u_h Xs + eta') D_12 + Xs DD_12 + a_rest Xs + b_rest)
         bnd2[m] = make_float4(ok ? a_rest : INFINITY, ok ? b_rest : INFINITY, eta1, 0.0f);
     }
@@ -225,9 +235,10 @@ __global__ __launch_bounds__(64) void pq_encode_exact_kernel(
 //     ||dx|| <= u_h Xs + eta sqrt(dsub)   (f16 rounding, denormals/flush),
 // with Dmax = max_ij ||c~_i - c~_j|| and DDmax = max_ij ||dc_i - dc_j|| measured on the
 // prepared image (pq_prep_mfma_kernel).  Per score, on top of that:
-//   E' = g_{dsub+2} (Cs^2/2 + 1.002 Xs Cs) + g_dsub Cs^2/2 + 2^-15 (Cs^2/2 + 1.002 Xs Cs)
+//   E' = g_{dsub+2} (Hs/2 + 1.002 Xs Cs) + g_dsub Hs/2 + 2^-15 (Hs/2 + 1.002 Xs Cs)
 //     (fp32 accumulation in any order, rounding of cn, the 8 index bits packed into the mantissa)
-//   canonical  |st*A_k - st*a_k| <= G/2 with G = (g_dsub + u) (Cs^2 + 2 Xs Cs)
+//   canonical  |st*A_k - st*a_k| <= G/2 with G = (g_dsub + u) (Hs + 2 Xs Cs)
+//   (Hs = sigma tau Cmax^2 bounds twice the accumulator init |cn| sigma tau / 2)
 //   => p_{k*} >= p_max - (||dx|| Dmax + Xs DDmax + 2E' + G).
 // W = a*Xs + b (pq_prep_mfma_kernel) includes a 1.0625 safety factor.
 constexpr int kWaves = 8;  // 512 threads: 2 waves per SIMD, 256 rows per workgroup

@@ -261,7 +261,7 @@ __global__ __launch_bounds__(kThreads) void pq_encode_cs_kernel(
     const float4 bm = bnd[m];
     const float sigma = bm.x;
     const float2v sig2 = {sigma, sigma};
-    const float xs_eta = 6.1035156e-5f * sqrtf((float)dsub);  // 2^-14 * sqrt(dsub)
+    const float xs_eta = 5.9604645e-8f * sqrtf((float)dsub);  // 2^-24 * sqrt(dsub) (pq.hip kEta)
     const uint32_t vmask = opaque_mask();
     unsigned char* stg = stg_all + w * 32 * PITCH;
     const int nvb = (nrows + 31) >> 5;
@@ -286,13 +286,23 @@ __global__ __launch_bounds__(kThreads) void pq_encode_cs_kernel(
     // right after staging it, so kDepth blocks per wave are in flight.
     auto step = [&](const int vb, float4 (&xr)[NIMAX]) __attribute__((always_inline)) {
         // sigma * x -> fp16 -> this wave's tile (LAYOUT 0: lanes past the block's rows skip)
+        // sigma == 1 (ordinary codebook magnitudes, pq_prep_mfma_kernel): no scaling multiply
+        if (sigma == 1.0f) {
 #pragma unroll
-        for (int i = 0; i < NIMAX; ++i) {
-            if (i < ni && (LAYOUT != 0 || (lactive && ibase(i) + prow[0] < 32))) {
-                const float2v lo = (float2v){xr[i].x, xr[i].y} * sig2;
-                const float2v hi = (float2v){xr[i].z, xr[i].w} * sig2;
-                *reinterpret_cast<uint2*>(stg + ibase(i) * PITCH + toff[i % PER]) =
-                    make_uint2(cvt2(lo.x, lo.y), cvt2(hi.x, hi.y));
+            for (int i = 0; i < NIMAX; ++i) {
+                if (i < ni && (LAYOUT != 0 || (lactive && ibase(i) + prow[0] < 32)))
+                    *reinterpret_cast<uint2*>(stg + ibase(i) * PITCH + toff[i % PER]) =
+                        make_uint2(cvt2(xr[i].x, xr[i].y), cvt2(xr[i].z, xr[i].w));
+            }
+        } else {
+#pragma unroll
+            for (int i = 0; i < NIMAX; ++i) {
+                if (i < ni && (LAYOUT != 0 || (lactive && ibase(i) + prow[0] < 32))) {
+                    const float2v lo = (float2v){xr[i].x, xr[i].y} * sig2;
+                    const float2v hi = (float2v){xr[i].z, xr[i].w} * sig2;
+                    *reinterpret_cast<uint2*>(stg + ibase(i) * PITCH + toff[i % PER]) =
+                        make_uint2(cvt2(lo.x, lo.y), cvt2(hi.x, hi.y));
+                }
             }
         }
         lds_fence();
@@ -382,7 +392,7 @@ __global__ __launch_bounds__(kThreads) void pq_encode_cs_kernel(
             top3_insert(t1, t2, t3, p2);
             top3_insert(t1, t2, t3, p3);
         }
-        // Xs >= ||sigma x||: |sigma x - x~| <= 2^-11 |sigma x| + 2^-14 per component
+        // Xs >= ||sigma x||: |sigma x - x~| <= 2^-11 |sigma x| + 2^-24 per component
         const float Xs = (sqrtf(xx) * (1.0f + 1e-5f) + xs_eta) * (1.0f + 9.765625e-4f);
         const float W = bm.y * Xs + bm.z;
         const float thr = t1 - W;
@@ -768,8 +778,8 @@ __global__ __launch_bounds__(kFWaves * 64) void pq_resolve_full_kernel(
 
     const float4 bm = bnd[m];
     const float2v sig2 = {bm.x, bm.x};
-    const float2v tau2 = sig2 * (float2v){4.0f, 4.0f};  // 2^kScaleC / 2^kScaleX
-    const float xs_eta = 6.1035156e-5f * sqrtf((float)dsub);
+    const float2v tau2 = {bm.w, bm.w};  // the image's scale (bnd.w)
+    const float xs_eta = 5.9604645e-8f * sqrtf((float)dsub);
     const float* cnm = cn + (int64_t)m * 256;
     const int q = dsub >> 2;
     const int nld = (32 * q + 63) >> 6;
@@ -962,7 +972,7 @@ __global__ __launch_bounds__(kFWaves * 64) __attribute__((amdgpu_waves_per_eu(2)
 
     const float4 bm = bnd[m];
     const float2v sig2 = {bm.x, bm.x};
-    const float xs_eta = 6.1035156e-5f * sqrtf((float)dsub);
+    const float xs_eta = 5.9604645e-8f * sqrtf((float)dsub);
     const float* cnm = cn + (int64_t)m * 256;
     const float* Cm = C + (int64_t)m * 256 * dsub;
     const half8* im = img + (int64_t)m * FR;

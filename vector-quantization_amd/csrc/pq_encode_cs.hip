@@ -182,8 +182,11 @@ constexpr int max_loads() {
 // loads after a wave's second vb (compute alone), 128 reads the same bytes as if x were
 // stored subspace-major (contiguous per workgroup: a memory-pattern probe), 256 settles full
 // items with the pair kernel's 256-wide exact scans instead of pq_resolve_full_kernel, 512
-// makes that kernel count (into `counts`) its rows, whole-row scans and candidates; with 512:
-// 1024 skips its exact chains, 2048 runs one filter block, 4096 gathers row 0 only.
+// makes the LDS-codebook full-item kernel count (into `counts`) its rows, whole-row scans and
+// candidates; with 512: 1024 skips its exact chains, 2048 runs one filter block, 4096 gathers
+// row 0 only.  Exact alternatives (same codes): 16384 the lane-wide top-3 filter instead of
+// the grouped top-2, 32768 no pair window in the pair kernel, 65536 the LDS-codebook
+// full-item kernel (pq_resolve_full_kernel) instead of pq_resolve_full2_kernel.
 // DS > 0: the kernel for sub-rows of exactly DS floats (the addresses and load counts fold
 // to constants); DS = 0 reads dsub at run time.
 template <int KS, int LAYOUT, int V = 0, int DS = 0>

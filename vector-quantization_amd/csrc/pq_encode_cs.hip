@@ -1142,6 +1142,41 @@ __global__ __launch_bounds__(256) void pq_transpose_codes_kernel(const uint8_t* 
     for (int e = threadIdx.x; e < rows * M; e += 256) codes[r0 * M + e] = tile[e];
 }
 
+// Same transpose with 16-B memory operations (n % 16 == 0 and 16-B aligned buffers): the
+// subspace rows come in as uint4 (16 codes), each thread assembles 16 output bytes from the
+// LDS tile ([M][256 + 16], padded) and stores them as one uint4.
+template <int MC>  // MC > 0: compile-time M (shifts instead of divisions)
+__global__ __launch_bounds__(256) void pq_transpose_codes16_kernel(const uint8_t* __restrict__ codesT, int64_t n,
+                                                                   int M_in, uint8_t* __restrict__ codes) {
+    const int M = MC > 0 ? MC : M_in;
+    extern __shared__ __attribute__((aligned(16))) uint8_t tile[];  // [M][272]
+    constexpr int TP = 256 + 16;
+    const int64_t r0 = (int64_t)blockIdx.x * 256;
+    const int rows = (int)min<int64_t>(256, n - r0);  // a multiple of 16
+    const int q = rows >> 4;                           // uint4 per subspace row
+    for (int e = threadIdx.x; e < M * q; e += 256) {
+        const int mm = e / q, c = e - mm * q;
+        *reinterpret_cast<uint4*>(tile + mm * TP + 16 * c) =
+            *reinterpret_cast<const uint4*>(codesT + (int64_t)mm * n + r0 + 16 * c);
+    }
+    __syncthreads();
+    const int nout = (rows * M) >> 4;  // uint4 of output
+    for (int e = threadIdx.x; e < nout; e += 256) {
+        uint32_t w[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            uint32_t v = 0;
+#pragma unroll
+            for (int b = 0; b < 4; ++b) {
+                const int o = 16 * e + 4 * j + b;  // output byte: row o / M, subspace o % M
+                v |= (uint32_t)tile[(o % M) * TP + o / M] << (8 * b);
+            }
+            w[j] = v;
+        }
+        *reinterpret_cast<uint4*>(codes + r0 * M + 16 * (int64_t)e) = make_uint4(w[0], w[1], w[2], w[3]);
+    }
+}
+
 int device_cus() {
     int dev = 0, cus = 0;
     if (hipGetDevice(&dev) != hipSuccess) return 256;
@@ -1260,8 +1295,17 @@ hipError_t launch_pq_encode_cs(int KS, const float* x, int64_t n, int d, int M, 
         default: return hipErrorInvalidValue;
     }
     if (e != hipSuccess) return e;
-    hipLaunchKernelGGL(pq_transpose_codes_kernel, dim3((unsigned)ceil_div(n, 256)), dim3(256), (size_t)256 * M, st,
-                       codesT, n, M, codes);
+    const bool v16 = n % 16 == 0 && (reinterpret_cast<uintptr_t>(codesT) % 16) == 0 &&
+                     (reinterpret_cast<uintptr_t>(codes) % 16) == 0 && M <= 256;
+    if (v16 && M == 16)
+        hipLaunchKernelGGL(pq_transpose_codes16_kernel<16>, dim3((unsigned)ceil_div(n, 256)), dim3(256),
+                           (size_t)(256 + 16) * M, st, codesT, n, M, codes);
+    else if (v16)
+        hipLaunchKernelGGL(pq_transpose_codes16_kernel<0>, dim3((unsigned)ceil_div(n, 256)), dim3(256),
+                           (size_t)(256 + 16) * M, st, codesT, n, M, codes);
+    else
+        hipLaunchKernelGGL(pq_transpose_codes_kernel, dim3((unsigned)ceil_div(n, 256)), dim3(256), (size_t)256 * M,
+                           st, codesT, n, M, codes);
     return hipGetLastError();
 }
 

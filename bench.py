@@ -254,9 +254,9 @@ def main():
                        "parallelism": f"row-sharded x{world}"},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic_from_profile(workload),
-                         "kernel": "mivq_pq_encode call: pq_encode_cs_kernel (filter) + pq_resolve_full_kernel and "
+                         "kernel": "mivq_pq_encode call: pq_encode_cs_kernel (filter) + pq_resolve_full2_kernel and "
                                    "pq_resolve_cs_kernel (exact re-check of the row-subspaces the filter could not "
-                                   "settle) + pq_transpose_codes_kernel",
+                                   "settle) + pq_transpose_codes16_kernel",
                          "bytes_per_vector": bytes_per_vec, "kernel_ms": kern_ms},
             "cpu_baseline": cpu,
             "parity_sample": parity,

@@ -114,6 +114,51 @@ def test_extrabitq_kernels_match_reference_fixture(dev, golden_dir, nbits):
     np.testing.assert_allclose(rec, e[f"{tag}_recon"], rtol=1e-5, atol=1e-6)
 
 
+def _prep_offsets(M, dsub, ksub=256):
+    """Byte offsets inside the mivq_pq_prepare buffer (mirror of PqPrepLayout, mivq_common.h)."""
+    al = lambda v: (v + 255) // 256 * 256  # noqa: E731
+    ks = (dsub + 15) // 16
+    L, off = {}, 0
+    for name, size in (("cn", 4 * M * ksub), ("ct", 4 * M * dsub * ksub), ("img", M * 8 * ks * 64 * 16),
+                       ("hinit", 4 * M * ksub), ("bnd", 16 * M), ("spread", 8 * M),
+                       ("pd", M * 256 * 256 * 8 if M <= 64 else 0), ("bnd2", 16 * M)):
+        L[name] = off
+        off = al(off + size)
+    return L
+
+
+@pytest.mark.parametrize("d,M", [(1536, 16), (1024, 16), (200, 4)])
+def test_pq_prep_spreads_bound_the_image(dev, d, M):
+    """The filter window rests on the measured spreads of the f16 image (pq_prep_spread_kernel):
+    Dmax^2 / DDmax^2 (fp32 chains) within (dsub + 3) 2^-24 of the fp64 value, and every
+    per-pair entry of pd an upper bound of the exact pair spread within 2e-5."""
+    from haag_vq import _native
+
+    rng = np.random.default_rng(11)
+    dsub = d // M
+    C = (rng.standard_normal((M, 256, dsub)) * rng.uniform(0.01, 3.0, (M, 1, 1))).astype(np.float32)
+    prep = _native.pq_prepare(_t(C, dev), 8)
+    torch.cuda.synchronize()
+    raw = _h(prep)
+    L = _prep_offsets(M, dsub)
+    spread = raw[L["spread"]:L["spread"] + 8 * M].view(np.float32).reshape(M, 2)
+    pd = raw[L["pd"]:L["pd"] + M * 256 * 256 * 8].view(np.float32).reshape(M, 256, 256, 2)
+    rel = (dsub + 3) * 2.0 ** -24 * 1.01
+    for m in range(M):
+        e = int(np.ceil(np.log2(np.abs(C[m]).max())))
+        t = (C[m] * np.float32(2.0 ** (14 - e))).astype(np.float32)
+        h = t.astype(np.float16).astype(np.float32)
+        r = (h - t).astype(np.float64)
+        h = h.astype(np.float64)
+        d1 = ((h[:, None, :] - h[None, :, :]) ** 2).sum(-1)
+        d2 = ((r[:, None, :] - r[None, :, :]) ** 2).sum(-1)
+        for got, ref in ((spread[m, 0], d1.max()), (spread[m, 1], d2.max())):
+            assert abs(float(got) - ref) <= rel * ref + 1e-30, (m, got, ref)
+        for k, ref in ((0, np.sqrt(d1)), (1, np.sqrt(d2))):
+            got = pd[m, :, :, k].astype(np.float64)
+            assert (got >= ref * (1 - 1e-7)).all() and (got <= ref * (1 + 2e-5) + 1e-30).all(), m
+
+
 def test_pq_encode_extreme_rows_fall_back_exactly(dev, oracle):
     """fp16 overflow (huge rows), NaN rows and zero rows take the exact fallback."""
     from haag_vq import _native

@@ -24,7 +24,8 @@ VARIANTS = {0: "encode + resolve", 1: "encode only", 2: "resolve: pairs only", 4
             17: "loads + convert + tile + fragments only", 65: "encode only, no x loads (compute alone)",
             145: "streaming only, subspace-major probe", 256: "encode + resolve, 256-wide full scans",
             513: "encode + full-item kernel", 1537: "... no exact chains", 2561: "... 1 of 8 filter blocks",
-            4609: "... no gathers", 7681: "... none of the three", 16384: "encode + resolve, lane-wide top-3 filter", 32768: "encode + resolve, no pair window", 65536: "encode + resolve, LDS-codebook full-item kernel"}
+            4609: "... no gathers", 7681: "... none of the three", 16384: "encode + resolve, lane-wide top-3 filter", 32768: "encode + resolve, no pair window", 65536: "encode + resolve, LDS-codebook full-item kernel",
+            131073: "encode only, A fragments of block 0 reused (LDS probe)", 131072: "encode + resolve, A fragments reused"}
 
 
 def prep_layout(M, dsub, ksub=256):

@@ -87,10 +87,27 @@ __global__ __launch_bounds__(256) void adc_lut_kernel(const float* __restrict__ 
         if (qq < nqb) lut[((q0 + qq) * M + m) * ksub + k] = l2 ? acc[qq] : -acc[qq];
 }
 
-// dist[qq] += entry qq of an (m, code) group of QB adjacent floats (16-B aligned for QB >= 4)
+// Position of entry qq of table group mk (= m*ksub + code) in the LDS table.  For QB = 8 the
+// two 16-B halves of a group are swapped when bit 3 of mk is set: a ds_read_b128 lane group
+// (16 lanes, random codes) then spreads its first reads over all 16 slots of the 256-B bank
+// row instead of the 8 even ones (expected 3.1 instead of 4.2 LDS cycles per lane group).
 template <int QB>
-__device__ __forceinline__ void lut_add(const float* g, float (&dist)[QB]) {
-    if constexpr (QB >= 4) {
+__device__ __forceinline__ int64_t tab_pos(int64_t mk, int qq) {
+    if constexpr (QB == 8) return mk * 8 + (qq ^ (int)((mk >> 1) & 4));
+    return mk * QB + qq;
+}
+
+// dist[qq] += entry qq of table group mk (QB adjacent floats, 16-B aligned for QB >= 4)
+template <int QB>
+__device__ __forceinline__ void lut_add(const float* tab, uint32_t mk, float (&dist)[QB]) {
+    const float* g = tab + (size_t)mk * QB;
+    if constexpr (QB == 8) {
+        const uint32_t s = (mk >> 1) & 4u;  // the halves are swapped when bit 3 of mk is set
+        const float4 t0 = *reinterpret_cast<const float4*>(g + s);
+        const float4 t1 = *reinterpret_cast<const float4*>(g + (s ^ 4u));
+        dist[0] += t0.x; dist[1] += t0.y; dist[2] += t0.z; dist[3] += t0.w;
+        dist[4] += t1.x; dist[5] += t1.y; dist[6] += t1.z; dist[7] += t1.w;
+    } else if constexpr (QB >= 4) {
 #pragma unroll
         for (int v = 0; v < QB / 4; ++v) {
             const float4 t = *reinterpret_cast<const float4*>(g + 4 * v);
@@ -122,7 +139,7 @@ __global__ __launch_bounds__(kScanWaves * 64) void adc_scan_kernel(
     for (int64_t e = tid; e < tab_elems * QB; e += kScanWaves * 64) {
         const int64_t mk = e / QB;
         const int qq = (int)(e - mk * QB);
-        tab[e] = qq < nqb ? lut[(q0 + qq) * tab_elems + mk] : 0.0f;
+        tab[tab_pos<QB>(mk, qq)] = qq < nqb ? lut[(q0 + qq) * tab_elems + mk] : 0.0f;
     }
     __syncthreads();
 
@@ -153,11 +170,11 @@ __global__ __launch_bounds__(kScanWaves * 64) void adc_scan_kernel(
 #pragma unroll
                     for (int b = 0; b < 4; ++b) {
                         const uint32_t code = (wrd >> (8 * b)) & 0xFFu;
-                        lut_add<QB>(tab + ((m0 + b) * ksub + code) * QB, dist);
+                        lut_add<QB>(tab, (uint32_t)((m0 + b) * ksub) + code, dist);
                     }
                 }
             } else {
-                for (int m = 0; m < M; ++m) lut_add<QB>(tab + (m * ksub + cr[m]) * QB, dist);
+                for (int m = 0; m < M; ++m) lut_add<QB>(tab, (uint32_t)(m * ksub + cr[m]), dist);
             }
         }
         const uint32_t gid = (uint32_t)(id_offset + row);
@@ -345,13 +362,23 @@ int adc_qb(int M, int ksub) {
     return 0;
 }
 
-// Row chunks per query block: about two workgroups per CU in total, at least one wave-step
-// of rows per wave.
+// Row chunks per query block.  The scan workgroups (16 waves, up to 128 KiB of LDS) run one
+// per CU, so the grid of nch * qblocks workgroups takes ceil(nch * qblocks / 256) rounds, each
+// as long as one workgroup's table fill (about half a wave-step of 1024 rows) plus its
+// ceil(n / nch / 1024) wave-steps: pick the nch of least total time (the smallest on ties:
+// fewer partial lists).  nq = 1000 at QB = 8, n = 1M: 2 chunks, 250 workgroups in one round,
+// instead of 625 in three of which the last is 44 % full.
 int64_t adc_chunks(int64_t nq, int64_t n, int QB) {
     const int64_t qblocks = ceil_div(nq, QB);
-    int64_t nch = ceil_div(512, qblocks);
-    nch = std::max<int64_t>(1, std::min<int64_t>(nch, ceil_div(n, 64 * kScanWaves)));
-    return nch;
+    const int64_t step_rows = 64 * kScanWaves;
+    const int64_t cap = std::max<int64_t>(1, std::min<int64_t>(1024, ceil_div(n, step_rows)));
+    int64_t best = 1;
+    double best_cost = 0.0;
+    for (int64_t nch = 1; nch <= cap; ++nch) {
+        const double cost = (double)ceil_div(nch * qblocks, 256) * ((double)ceil_div(ceil_div(n, nch), step_rows) + 0.5);
+        if (nch == 1 || cost < best_cost * (1.0 - 1e-9)) { best = nch; best_cost = cost; }
+    }
+    return best;
 }
 
 template <int R, int QB>

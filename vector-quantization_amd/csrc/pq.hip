@@ -79,36 +79,59 @@ __device__ int subspace_scale_exp(const float* Cm, int dsub, float* red) {
 // Pairwise spreads of the prepared image of subspace m (the window derivation above
 // pq_encode_mfma_kernel):  Dmax = max_ij ||c~_i - c~_j||,  DDmax = max_ij ||dc_i - dc_j||,
 // c~ = f16(tau c), dc = c~ - tau c (exact in fp32).  Grid (M, 16): block (m, g) takes rows
-// i in [16g, 16g + 16) against all 256 j, one fp32 chain per pair (relative rounding of a
+// i in [16g, 16g + 16) against all 256 j (the image staged in LDS by 32-dimension chunks),
+// one fp32 chain per pair (relative rounding of a
 // squared sum <= (dsub + 3) 2^-24, covered by the (1 + 1e-5) applied to the norms); the
 // maxima of the squared sums go to spread[m] with atomicMax on their bits (non-negative).
+constexpr int kSpreadTC = 32;  // dimensions per LDS chunk of the spread kernel
+
 __global__ __launch_bounds__(256) void pq_prep_spread_kernel(const float* __restrict__ C, int dsub,
                                                              uint32_t* __restrict__ spread, float2* __restrict__ pd) {
+    // the image of all 256 centroids for kSpreadTC dimensions at a time: (c~, c~ - tau c) per
+    // element, rows padded to an odd number of float2 (the 16 j rows a lane group reads sit on
+    // distinct banks)
+    __shared__ float2 img[256][kSpreadTC + 1];
     __shared__ float red[256];
     const int m = blockIdx.x, g = blockIdx.y, tid = threadIdx.x;
     const float* Cm = C + (int64_t)m * 256 * dsub;
     const float tau = ldexpf(1.0f, kScaleC - subspace_scale_exp(Cm, dsub, red));
-    const int i = 16 * g + (tid >> 4);
-    const float* ci = Cm + (int64_t)i * dsub;
-    float d1 = 0.0f, d2 = 0.0f;
-    for (int jj = 0; jj < 16; ++jj) {
-        const float* cj = Cm + (int64_t)(16 * jj + (tid & 15)) * dsub;
-        float s1 = 0.0f, s2 = 0.0f;
-        for (int t = 0; t < dsub; ++t) {
-            const float ti = tau * ci[t], tj = tau * cj[t];
-            const float hi = (float)(_Float16)ti, hj = (float)(_Float16)tj;
-            const float dc = (hi - ti) - (hj - tj);
-            const float dh = hi - hj;
-            s1 = __builtin_fmaf(dh, dh, s1);
-            s2 = __builtin_fmaf(dc, dc, s2);
+    const int il = 16 * g + (tid >> 4), jl = tid & 15;
+    float s1[16], s2[16];
+#pragma unroll
+    for (int jj = 0; jj < 16; ++jj) s1[jj] = s2[jj] = 0.0f;
+    for (int t0 = 0; t0 < dsub; t0 += kSpreadTC) {
+        const int tc = min(kSpreadTC, dsub - t0);
+        __syncthreads();
+        for (int e = tid; e < 256 * kSpreadTC; e += 256) {
+            const int k = e / kSpreadTC, t = e - k * kSpreadTC;
+            if (t < tc) {
+                const float ti = tau * Cm[(int64_t)k * dsub + t0 + t];
+                const float hi = (float)(_Float16)ti;
+                img[k][t] = make_float2(hi, hi - ti);
+            }
         }
-        // NaN pairs (a NaN centroid never wins, and its filter score is never a candidate)
-        // are skipped by fmaxf; inf gives inf -> the window is infinite
-        d1 = fmaxf(d1, s1);
-        d2 = fmaxf(d2, s2);
+        __syncthreads();
+        for (int t = 0; t < tc; ++t) {
+            const float2 a = img[il][t];
+#pragma unroll
+            for (int jj = 0; jj < 16; ++jj) {
+                const float2 b = img[16 * jj + jl][t];
+                const float dh = a.x - b.x, dc = a.y - b.y;
+                s1[jj] = __builtin_fmaf(dh, dh, s1[jj]);
+                s2[jj] = __builtin_fmaf(dc, dc, s2[jj]);
+            }
+        }
+    }
+    // NaN pairs (a NaN centroid never wins, and its filter score is never a candidate) are
+    // skipped by fmaxf; inf gives inf -> the window is infinite
+    float d1 = 0.0f, d2 = 0.0f;
+#pragma unroll
+    for (int jj = 0; jj < 16; ++jj) {
+        d1 = fmaxf(d1, s1[jj]);
+        d2 = fmaxf(d2, s2[jj]);
         if (pd)  // the pair's own spreads (NaN stays NaN: the pair window then never settles it)
-            pd[((int64_t)m * 256 + i) * 256 + 16 * jj + (tid & 15)] =
-                make_float2(sqrtf(s1) * (1.0f + 1e-5f), sqrtf(s2) * (1.0f + 1e-5f));
+            pd[((int64_t)m * 256 + il) * 256 + 16 * jj + jl] =
+                make_float2(sqrtf(s1[jj]) * (1.0f + 1e-5f), sqrtf(s2[jj]) * (1.0f + 1e-5f));
     }
     atomicMax(&spread[2 * m + 0], __float_as_uint(d1));
     atomicMax(&spread[2 * m + 1], __float_as_uint(d2));

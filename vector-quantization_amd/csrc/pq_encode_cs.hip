@@ -186,7 +186,8 @@ constexpr int max_loads() {
 // candidates; with 512: 1024 skips its exact chains, 2048 runs one filter block, 4096 gathers
 // row 0 only.  Exact alternatives (same codes): 16384 the lane-wide top-3 filter instead of
 // the grouped top-2, 32768 no pair window in the pair kernel, 65536 the LDS-codebook
-// full-item kernel (pq_resolve_full_kernel) instead of pq_resolve_full2_kernel.
+// full-item kernel (pq_resolve_full_kernel) instead of pq_resolve_full2_kernel.  131072 (wrong
+// codes): every centroid block reuses block 0's A fragments (an LDS-read probe).
 // DS > 0: the kernel for sub-rows of exactly DS floats (the addresses and load counts fold
 // to constants); DS = 0 reads dsub at run time.
 template <int KS, int LAYOUT, int V = 0, int DS = 0>
@@ -340,7 +341,7 @@ __global__ __launch_bounds__(kThreads) void pq_encode_cs_kernel(
         auto scores = [&](int cb) __attribute__((always_inline)) {
             half8 a[KS];
 #pragma unroll
-            for (int ks = 0; ks < KS; ++ks) a[ks] = cimg[(cb * KS + ks) * 64 + l];
+            for (int ks = 0; ks < KS; ++ks) a[ks] = cimg[(((V & 131072) ? 0 : cb) * KS + ks) * 64 + l];
             floatx16 acc;
 #pragma unroll
             for (int qq = 0; qq < 4; ++qq) {

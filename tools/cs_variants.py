@@ -65,6 +65,8 @@ def main():
     ap.add_argument("--data", default="clustered")
     ap.add_argument("--ab", default="", help="V1,V2: interleaved A/B timing instead of the variant table")
     ap.add_argument("--lib", default="", help="prebuilt harness library (e.g. another MIVQ_CS_WAVES)")
+    ap.add_argument("--ab-lib", default="", help="other harness library: interleaved A/B of V=--ab-v in both")
+    ap.add_argument("--ab-v", type=int, default=0)
     a = ap.parse_args()
     lib = build(a.lib)
     dev = _native.require_device()
@@ -83,7 +85,7 @@ def main():
     st = torch.cuda.current_stream().cuda_stream
     P = ctypes.c_void_p
 
-    def run(v):
+    def run(v, lib=lib):
         rc = lib.cs_variant(ctypes.c_int(v), P(X.data_ptr()), ctypes.c_int64(a.n), ctypes.c_int(a.d), ctypes.c_int(a.M),
                             ctypes.c_int(dsub), P(C.data_ptr()), P(base + L["cn"]), P(base + L["img"]),
                             P(base + L["hinit"]), P(base + L["bnd"]), P(base + L["pd"]), P(base + L["bnd2"]),
@@ -91,6 +93,33 @@ def main():
                             P(st))
         assert rc == 0, rc
 
+    if a.ab_lib:
+        libs = {"this": lib, a.ab_lib: ctypes.CDLL(str(ROOT / a.ab_lib))}
+        res = {k: [] for k in libs}
+        for k, lb in libs.items():
+            run(a.ab_v, lb)
+        torch.cuda.synchronize()
+        for _ in range(a.reps * 3):
+            for k, lb in libs.items():
+                s_, e_ = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                s_.record(); run(a.ab_v, lb); e_.record()
+                torch.cuda.synchronize()
+                res[k].append(s_.elapsed_time(e_))
+        for k in libs:
+            t = sorted(res[k])
+            print(f"AB lib={k} V={a.ab_v}: median {t[len(t) // 2]:.3f} ms  min {t[0]:.3f}  max {t[-1]:.3f}", flush=True)
+        # back-to-back (no idle gap: the power-managed clock of a sustained run)
+        for k, lb in libs.items():
+            s_, e_ = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            for _ in range(3):
+                run(a.ab_v, lb)
+            s_.record()
+            for _ in range(20):
+                run(a.ab_v, lb)
+            e_.record()
+            torch.cuda.synchronize()
+            print(f"AB lib={k} V={a.ab_v}: back-to-back {s_.elapsed_time(e_) / 20:.3f} ms/call", flush=True)
+        return
     if a.ab:
         va, vb = (int(t) for t in a.ab.split(","))
         res = {va: [], vb: []}
@@ -119,6 +148,11 @@ def main():
     rows = int((diff[:, 0] & 0xFFFF).sum()); scans = int((diff[:, 0] >> 16).sum()); cands = int((diff[:, 1] >> 8).sum())
     print(f"full kernel: rows {rows}, whole-row scans {scans}, candidates {cands} ({cands / max(rows, 1):.2f}/row)",
           flush=True)
+    run(262144)
+    torch.cuda.synchronize()
+    st_, ga_ = (int(v) for v in counts.long().sum(0).tolist())
+    print(f"pair kernel: {st_} pairs settled by the pair window, {ga_} gathered "
+          f"({st_ / max(st_ + ga_, 1):.1%} settled)", flush=True)
     for v, name in VARIANTS.items():
         run(v)
         torch.cuda.synchronize()

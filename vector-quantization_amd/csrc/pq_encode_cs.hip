@@ -187,7 +187,9 @@ constexpr int max_loads() {
 // row 0 only.  Exact alternatives (same codes): 16384 the lane-wide top-3 filter instead of
 // the grouped top-2, 32768 no pair window in the pair kernel, 65536 the LDS-codebook
 // full-item kernel (pq_resolve_full_kernel) instead of pq_resolve_full2_kernel.  131072 (wrong
-// codes): every centroid block reuses block 0's A fragments (an LDS-read probe).
+// codes): every centroid block reuses block 0's A fragments (an LDS-read probe).  262144 (codes
+// exact): the pair kernel stores (pairs settled by the pair window, pairs gathered) per
+// workgroup into `counts`.
 // DS > 0: the kernel for sub-rows of exactly DS floats (the addresses and load counts fold
 // to constants); DS = 0 reads dsub at run time.
 template <int KS, int LAYOUT, int V = 0, int DS = 0>
@@ -252,9 +254,9 @@ __global__ __launch_bounds__(kThreads) void pq_encode_cs_kernel(
         toff[sidx] = prow[sidx] * PITCH + 8 * col;
     }
     if (LAYOUT == 0) lactive = l < rpi * q;
-    // Buffer over this workgroup's rows of subspace m.  The whole byte offset goes in the
-    // (range-checked) VGPR offset, so rows past the range read as zeros without a branch;
-    // idle lanes of LAYOUT 0 get an offset >= 2^31, past any range.
+    // Buffer over this workgroup's rows of subspace m.  voffset + soffset is range-checked, so
+    // rows past the range read as zeros without a branch; idle lanes of LAYOUT 0 get a
+    // voffset >= 2^31, past any range.
     const __amdgpu_buffer_rsrc_t xr_rsrc = __builtin_amdgcn_make_buffer_rsrc(
         (void*)(x + ((V & 128) ? ((int64_t)m * n + r0) * dsub : r0 * d + (int64_t)m * dsub)), 0,
         (int)(((int64_t)(nrows - 1) * XS + dsub) * 4), kRsrcWord3);
@@ -278,8 +280,10 @@ __global__ __launch_bounds__(kThreads) void pq_encode_cs_kernel(
 #pragma unroll
         for (int i = 0; i < NIMAX; ++i) {
             if (i < ni) {  // uniform
-                const uint32_t vo = (uint32_t)voff[i % PER] + (uint32_t)((vb * 32 + ibase(i)) * XS * 4);
-                const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(xr_rsrc, (int)vo, 0, kXAux);
+                // the block's uniform offset goes in soffset (SALU; gfx950 range-checks
+                // voffset + soffset, tools/probes/soffset_range.hip), the lane's in voffset
+                const int so = (vb * 32 + ibase(i)) * XS * 4;
+                const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(xr_rsrc, voff[i % PER], so, kXAux);
                 dst[i] = make_float4(__uint_as_float(v[0]), __uint_as_float(v[1]), __uint_as_float(v[2]),
                                      __uint_as_float(v[3]));
             }
@@ -514,6 +518,7 @@ __global__ __launch_bounds__(kRWaves * 64) void pq_resolve_cs_kernel(
         }
         if (tid < 256) cnl[tid] = cn[(int64_t)m * 256 + tid];
         if (tid == 0) ctr[0] = 0;
+        if ((V & 262144) && tid == 0) ctr[1] = ctr[2] = 0;
     }
     __syncthreads();
 
@@ -652,6 +657,7 @@ __global__ __launch_bounds__(kRWaves * 64) void pq_resolve_cs_kernel(
             // compact the remaining items into lanes 0 .. cntb-1
             const uint64_t km = __ballot(keep);
             const int cntb = __popcll(km);
+            if ((V & 262144) && l == 0) { atomicAdd(&ctr[1], cnt0 - cntb); atomicAdd(&ctr[2], cntb); }
             uint2* comp = comp_all + w * 64;
             if (keep) comp[__popcll(km & ((1ull << l) - 1ull))] = it;
             lds_fence();
@@ -705,6 +711,10 @@ __global__ __launch_bounds__(kRWaves * 64) void pq_resolve_cs_kernel(
             const float s2 = __builtin_fmaf(-2.0f, d2, cnl[k2]);
             codesT[(int64_t)m * n + r0 + rowl] = (uint8_t)((s2 < s1 || (s2 == s1 && k2 < k1)) ? k2 : k1);
         }
+    }
+    if constexpr ((V & 262144) != 0) {  // instrumentation: pairs settled by the pair window / gathered
+        __syncthreads();
+        if (tid == 0) const_cast<int2*>(counts)[blockIdx.x] = make_int2(ctr[1], ctr[2]);
     }
 }
 

@@ -120,8 +120,12 @@ __device__ __forceinline__ float load_f32(const unsigned char* p) {
 
 constexpr int kEstWaves = 8;  // waves per workgroup (all share the query block in LDS)
 constexpr int kEstTiles = 4;  // 32-code tiles per wave (each workgroup: 8 waves x 128 codes)
+constexpr int kEstRegG = 24;  // 16-B groups of a code row held in registers (d <= 3072)
 
-// Grid (ceil(m / (32 kEstWaves kEstTiles)), ceil(nq / 32)), 512 threads.  LDS holds only the
+// Grid nqb * ceil(m / (32 kEstWaves kEstTiles)) (nqb = ceil(nq / 32)), 512 threads; the query
+// block index runs fastest, so the nqb workgroups reading one chunk of codes run side by side
+// and all but the first find it in L2 / MALL (the codes are read from HBM about once instead of
+// once per query block).  LDS holds only the
 // 32 query rows (int8, pitch d + 16), so two workgroups fit a CU up to d = 2048 and one up to
 // d = 4096.  Lane (r, h) of a wave owns code r of the tile and, per 32-dim k-step s, the 16
 // sign bits of dims 32s + 16h .. +16: the low (h = 0) or high half of the row's dword s, read
@@ -129,13 +133,14 @@ constexpr int kEstTiles = 4;  // 32-code tiles per wave (each workgroup: 8 waves
 // factors of code r move to the accumulator lanes by shuffles.
 __global__ __launch_bounds__(kEstWaves * 64) void rabitq_est_mfma_kernel(
     const uint8_t* __restrict__ codes, int64_t m, int d, const int8_t* __restrict__ qq, const float* __restrict__ qf,
-    int64_t nq, int metric, float* __restrict__ buf) {
+    int64_t nq, int metric, float* __restrict__ buf, unsigned nqb) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     const int nb = d >> 3, cs = nb + 8;  // d % 32 == 0: cs % 4 == 0
     const int QP = d + 16;
     int8_t* qs = reinterpret_cast<int8_t*>(smem);
     const int tid = threadIdx.x, w = tid >> 6, l = tid & 63, r = l & 31, h = l >> 5;
-    const int64_t q0 = (int64_t)blockIdx.y * 32;
+    const unsigned qblk = blockIdx.x % nqb, cchunk = blockIdx.x / nqb;
+    const int64_t q0 = (int64_t)qblk * 32;
     const int qch = d >> 4;
     for (int e = tid; e < 32 * qch; e += kEstWaves * 64) {
         const int row = e / qch, c = e - row * qch;
@@ -156,8 +161,30 @@ __global__ __launch_bounds__(kEstWaves * 64) void rabitq_est_mfma_kernel(
     const int nks = d >> 5;  // k-steps; nks % 4 handled by the dword tail
     const int8_t* qrow = qs + r * QP + 16 * h;
     const int sh = 16 * h;
+    const int n4 = nks >> 2;
+    // d <= 32 * 4 * kEstRegG: a tile's code bits (n4 16-B loads per lane) are all issued at once,
+    // the next tile's right after the last k-step of this one (before the epilogue), so each
+    // tile waits for memory about once instead of once per 16-B group
+    const bool inreg = n4 <= kEstRegG;
+    u32x4a4 cg[kEstRegG];
+    auto tile_row = [&](int t, int& nc) -> const uint8_t* {
+        const int64_t cb = (((int64_t)cchunk * kEstWaves + w) * kEstTiles + t) * 32;
+        nc = (int)max<int64_t>(0, min<int64_t>(32, m - cb));
+        // rows past the chunk read row 0 of the tile (in range) and are never written
+        return codes + (cb + (r < nc ? r : 0)) * cs;
+    };
+    auto load_tile = [&](const uint8_t* crow) __attribute__((always_inline)) {
+#pragma unroll
+        for (int g = 0; g < kEstRegG; ++g)
+            if (g < n4) cg[g] = *reinterpret_cast<const u32x4a4*>(crow + 16 * g);
+    };
+    if (inreg) {
+        int nc0;
+        const uint8_t* row0 = tile_row(0, nc0);
+        if (nc0 > 0) load_tile(row0);
+    }
     for (int t = 0; t < kEstTiles; ++t) {
-        const int64_t cb = (((int64_t)blockIdx.x * kEstWaves + w) * kEstTiles + t) * 32;
+        const int64_t cb = (((int64_t)cchunk * kEstWaves + w) * kEstTiles + t) * 32;
         if (cb >= m) break;  // wave-uniform
         const int nc = (int)min<int64_t>(32, m - cb);
         // rows past the chunk read row 0 of the tile (in range) and are never written
@@ -173,8 +200,17 @@ __global__ __launch_bounds__(kEstWaves * 64) void rabitq_est_mfma_kernel(
             const v4i bq = *reinterpret_cast<const v4i*>(qrow + 32 * s);
             acc = __builtin_amdgcn_mfma_i32_32x32x32_i8(av, bq, acc, 0, 0, 0);
         };
-        const int n4 = nks >> 2;
-        if (n4 > 0) {
+        if (inreg) {
+#pragma unroll
+            for (int g = 0; g < kEstRegG; ++g) {
+                if (g < n4) {
+                    kstep(cg[g][0], 4 * g + 0);
+                    kstep(cg[g][1], 4 * g + 1);
+                    kstep(cg[g][2], 4 * g + 2);
+                    kstep(cg[g][3], 4 * g + 3);
+                }
+            }
+        } else if (n4 > 0) {
             u32x4a4 cur = *reinterpret_cast<const u32x4a4*>(crow);  // cs % 4 == 0: 4-B aligned rows
             for (int g = 0; g < n4; ++g) {
                 const u32x4a4 nxt = g + 1 < n4 ? *reinterpret_cast<const u32x4a4*>(crow + 16 * (g + 1)) : cur;
@@ -187,6 +223,11 @@ __global__ __launch_bounds__(kEstWaves * 64) void rabitq_est_mfma_kernel(
         }
         for (int s = 4 * n4; s < nks; ++s) kstep(*reinterpret_cast<const uint32_t*>(crow + 4 * s), s);
         const float fr = *reinterpret_cast<const float*>(crow + nb + 4 * h);  // h = 0: f0, h = 1: f1 of code r
+        if (inreg && t + 1 < kEstTiles) {
+            int nc1;
+            const uint8_t* nrow = tile_row(t + 1, nc1);
+            if (nc1 > 0) load_tile(nrow);
+        }
         // every lane takes part in the shuffles (a bpermute from an inactive lane reads 0);
         // only the stores are guarded
         float* orow = buf + (qok ? qa : 0) * m + cb;
@@ -305,9 +346,10 @@ extern "C" int mivq_rabitq_search(const uint8_t* codes, int64_t n, int32_t d, co
         nq, n, k, id_offset, p + L.tiled, dists, ids, st, [&](int64_t c0, int64_t m, float* buf) {
             const uint8_t* cc = codes + c0 * nbytes;
             if (mfma)
-                hipLaunchKernelGGL(rabitq_est_mfma_kernel, dim3((unsigned)ceil_div(m, kEstWaves * kEstTiles * 32),
-                                                                (unsigned)ceil_div(nq, 32)),
-                                   dim3(kEstWaves * 64), smem, st, cc, m, d, qq, qf, nq, metric, buf);
+                hipLaunchKernelGGL(rabitq_est_mfma_kernel,
+                                   dim3((unsigned)(ceil_div(m, kEstWaves * kEstTiles * 32) * ceil_div(nq, 32))),
+                                   dim3(kEstWaves * 64), smem, st, cc, m, d, qq, qf, nq, metric, buf,
+                                   (unsigned)ceil_div(nq, 32));
             else
                 hipLaunchKernelGGL(rabitq_est_generic_kernel, dim3((unsigned)ceil_div(m, 256), (unsigned)nq),
                                    dim3(256), 0, st, cc, m, d, qq, qr, qf, qb, metric, buf);

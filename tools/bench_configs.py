@@ -95,7 +95,7 @@ def run_opq32(a, dev):
         "metric": "OPQ32 encode vectors/sec + ADC queries/sec @ recall@10, 1M×1536 fp32 (BASELINE configs[2])",
         "value": a.n / wall, "unit": "vectors/s", "ms_per_step": wall * 1e3, "dtype": "f32",
         "config": {"workload": f"opq32_encode_{a.n}x{d}", "M": M, "nbits": 8, "opq_outer_iters": a.opq_iters},
-        "roofline": {"bound": "mfma", "kernel": "opq_rotate (fp32 MFMA 32x32x2)", "achieved": flops / (rot_ms * 1e-3) / 1e12,
+        "roofline": {"bound": "mfma", "kernel": "mivq_opq_rotate (rocBLAS fp32 sgemm)", "achieved": flops / (rot_ms * 1e-3) / 1e12,
                      "peak": MFMA_F32_PEAK_TFS, "unit": "TFLOP/s", "frac": flops / (rot_ms * 1e-3) / 1e12 / MFMA_F32_PEAK_TFS,
                      "rotate_ms": rot_ms, "encode_call_ms": dev_ms - rot_ms},
         "adc": {"qps": a.nq / swall, "nq": a.nq, "k": 10, "recall@10": rec, "recall_queries": 100,

@@ -9,6 +9,18 @@
 // precision).  128x128 output tile per 256-thread workgroup, 2x2 32x32 tiles per wave,
 // BK = 16 slices of x and A staged through LDS (k-major so every fragment read is a
 // contiguous, conflict-free 128-B row).
+//
+// mivq_opq_rotate itself runs the library fp32 GEMM (rocBLAS sgemm on the caller's stream,
+// 147 TFLOP/s at 1M x 1536 against 56 for opq_gemm_kernel — tools/dbg/gemm_probe.py): the
+// rotation is a plain GEMM with nothing to fuse.  MIVQ_OPQ_NATIVE_GEMM=1 selects the kernel
+// below instead; it also serves when rocBLAS reports an error.
+#include <rocblas/rocblas.h>
+
+#include <algorithm>
+#include <cstdlib>
+#include <map>
+#include <mutex>
+
 #include "mivq_common.h"
 
 namespace mivq {
@@ -88,6 +100,48 @@ __global__ __launch_bounds__(256) void opq_gemm_kernel(const float* __restrict__
 }  // namespace
 }  // namespace mivq
 
+namespace mivq {
+namespace {
+
+// One rocBLAS handle per device, created on first use and kept for the process.
+rocblas_handle blas_handle() {
+    static std::mutex mu;
+    static std::map<int, rocblas_handle> handles;
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess) return nullptr;
+    std::lock_guard<std::mutex> lk(mu);
+    auto it = handles.find(dev);
+    if (it != handles.end()) return it->second;
+    rocblas_handle h = nullptr;
+    if (rocblas_create_handle(&h) != rocblas_status_success) return nullptr;
+    handles[dev] = h;
+    return h;
+}
+
+// y (n x d, row-major) = x . A^T (transpose 0) or x . A (transpose 1).  Column-major view:
+// Y^T = op(A_cm) . X^T with A_cm = A^T as stored, so op = T for x . A^T and N for x . A.
+bool rotate_blas(const float* x, int64_t n, int d, const float* A, int transpose, float* y, hipStream_t st) {
+    static const bool native = [] {
+        const char* e = std::getenv("MIVQ_OPQ_NATIVE_GEMM");
+        return e && e[0] == '1';
+    }();
+    if (native) return false;
+    rocblas_handle h = blas_handle();
+    if (!h || rocblas_set_stream(h, st) != rocblas_status_success) return false;
+    const float one = 1.0f, zero = 0.0f;
+    const int64_t step = (int64_t)1 << 30;  // rocblas_int columns per call
+    for (int64_t r = 0; r < n; r += step) {
+        const int cols = (int)std::min<int64_t>(step, n - r);
+        if (rocblas_sgemm(h, transpose ? rocblas_operation_none : rocblas_operation_transpose, rocblas_operation_none,
+                          d, cols, d, &one, A, d, x + r * d, d, &zero, y + r * d, d) != rocblas_status_success)
+            return false;
+    }
+    return true;
+}
+
+}  // namespace
+}  // namespace mivq
+
 using namespace mivq;
 
 extern "C" int mivq_opq_rotate(const float* x, int64_t n, int32_t d, const float* A, int32_t transpose, float* y,
@@ -96,6 +150,7 @@ extern "C" int mivq_opq_rotate(const float* x, int64_t n, int32_t d, const float
     MIVQ_REQUIRE(transpose == 0 || transpose == 1, MIVQ_ERR_INVALID, "opq_rotate: transpose must be 0 or 1");
     if (n == 0) return MIVQ_OK;
     MIVQ_REQUIRE(x && A && y && x != y, MIVQ_ERR_INVALID, "opq_rotate: null or aliased pointer");
+    if (mivq::rotate_blas(x, n, d, A, transpose, y, as_stream(stream))) return check_launch("opq_rotate (rocBLAS)");
     const dim3 grid((unsigned)ceil_div(n, BM), (unsigned)ceil_div(d, BN));
     hipLaunchKernelGGL(opq_gemm_kernel, grid, dim3(256), 0, as_stream(stream), x, n, d, A, transpose, y);
     return check_launch("opq_rotate");

@@ -11,7 +11,7 @@ Drop-in for the reference's ``OptimizedProductQuantizer``
   then train a fresh PQ on the rotated data (:26-28).
 * compress = PQ encode of x . A^T (:31); decompress = PQ decode . A (:34).
 
-Hot path on device: the rotation is ``mivq_opq_rotate`` (exact-f32 MFMA GEMM), encode /
+Hot path on device: the rotation is ``mivq_opq_rotate`` (fp32 GEMM, rocBLAS sgemm), encode /
 decode are the PQ kernels.  The Procrustes step of training (a D x D product and SVD) uses
 the vendor libraries through torch — it is training, not the encode path.
 """

@@ -125,7 +125,7 @@ def cpu_baseline(X: torch.Tensor, C: np.ndarray, codes_dev: torch.Tensor, target
         "unit": "vectors/s",
         "cores": threads,
         "kind": "port",
-        "sample": f"first {n_s} rows of rank 0's shard, oracle/mivq_oracle.c pq_encode (OpenMP, AVX2), {dt:.1f} s",
+        "sample": f"first {n_s} rows of rank 0's shard, oracle/mivq_oracle.c pq_encode (OpenMP, AVX2), {dt:.1f} s wall on {threads} threads = {dt * threads:.0f} thread-s",
     }, {"rows_checked": n_s, "mismatched_codes": mism}
 
 

@@ -129,15 +129,22 @@ def pq_encode_fp64(X: np.ndarray, C: np.ndarray):
     codes = np.empty((n, M), np.uint8)
     gap = np.empty((n, M), np.float64)
     for m in range(M):
-        dist = ((Xs[:, m, None, :] - C[None, m]) ** 2).sum(-1)  # (n, ksub)
-        order = np.argsort(dist, axis=1, kind="stable")
-        codes[:, m] = order[:, 0]
+        # |x|^2 + |c|^2 - 2 x.c in fp64 (BLAS): its rounding (~1e-15 of the scale) is far
+        # below any gap this is used to certify (>= 1e-5 of the scale)
+        xx = (Xs[:, m] ** 2).sum(-1)
+        cc = (C[m] ** 2).sum(-1)
+        dist = xx[:, None] + cc[None, :] - 2.0 * (Xs[:, m] @ C[m].T)  # (n, ksub)
         if ksub > 1:
-            d0 = dist[np.arange(n), order[:, 0]]
-            d1 = dist[np.arange(n), order[:, 1]]
-            scale = (Xs[:, m] ** 2).sum(-1) + (C[m] ** 2).sum(-1).max()
+            top2 = np.argpartition(dist, 1, axis=1)[:, :2]
+            d2 = np.take_along_axis(dist, top2, 1)
+            first = np.where(d2[:, 0] <= d2[:, 1], 0, 1)
+            codes[:, m] = top2[np.arange(n), first]
+            d0 = d2[np.arange(n), first]
+            d1 = d2[np.arange(n), 1 - first]
+            scale = xx + cc.max()
             gap[:, m] = (d1 - d0) / np.maximum(scale, 1e-300)
         else:
+            codes[:, m] = 0
             gap[:, m] = np.inf
     return codes, gap
 

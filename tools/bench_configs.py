@@ -1,4 +1,5 @@
-"""Throughput of the other BASELINE.json configs on 1 GPU (bench.py measures the headline PQ16).
+"""Throughput of the other BASELINE.json configs on 1 GPU, one at a time (bench.py runs the
+opq32 / sq8 / rabitq1 legs itself as its `configs` key; ivfpq lives only here).
 
 usage: python tools/bench_configs.py --workload opq32|sq8|rabitq1|ivfpq [--n N] [--steps K] [--warmup W]
 
@@ -27,7 +28,7 @@ ROOT = Path(__file__).resolve().parent.parent
 sys.path.insert(0, str(ROOT / "vector-quantization_amd"))
 sys.path.insert(0, str(ROOT))
 from haag_vq import _native  # noqa: E402
-from bench import synth, log  # noqa: E402
+from bench import synth, log, opq32_leg, flatcodes_leg  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0
 MFMA_F32_PEAK_TFS = 157.3  # MI355X dense fp32 matrix (MI355X_MICROARCH.md chip table)
@@ -51,111 +52,6 @@ def timed(fn, steps, warmup):
 
 def recall(gt_ids, got_ids, k):
     return float(np.mean([len(set(gt_ids[j][:k]) & set(got_ids[j][:k])) / k for j in range(len(gt_ids))]))
-
-
-def run_opq32(a, dev):
-    from haag_vq.methods.optimized_product_quantization import OptimizedProductQuantizer
-
-    d, M = 1536, 32
-    X = synth(a.n, d, seed=0, dev=dev, kind="clustered")
-    t0 = time.perf_counter()
-    opq = OptimizedProductQuantizer(M=M, B=8)
-    opq.niter = a.opq_iters
-    opq.fit(X[:65536])
-    torch.cuda.synchronize()
-    log(f"OPQ fit on 65536 rows ({a.opq_iters} outer iterations): {time.perf_counter() - t0:.1f} s")
-    A = opq.opq.A_device
-    pq = opq.inner
-    C = pq.centroids_device
-    prep = _native.pq_prepare(C, 8)
-    Y = torch.empty_like(X)
-    codes = torch.empty((a.n, M), dtype=torch.uint8, device=dev)
-
-    def rot():
-        _native.opq_rotate(X, A, False, out=Y)
-
-    def step():
-        rot()
-        _native.pq_encode(Y, C, prep, 8, out=codes)
-
-    wall, dev_ms = timed(step, a.steps, a.warmup)
-    _, rot_ms = timed(rot, a.steps, 1)
-    Q = synth(a.nq, d, seed=1_000_003, dev=dev, kind="clustered")
-
-    def search():
-        lut = _native.adc_lut(_native.opq_rotate(Q, A, False), C, 8)
-        return _native.adc_search(lut, codes, 10, 8)
-
-    swall, sdev = timed(search, 3, 1)
-    _, ai = search()
-    _, gi = _native.flat_search(Q[:100].contiguous(), X, 10)
-    rec = recall(gi.cpu().numpy(), ai[:100].cpu().numpy(), 10)
-    flops = 2.0 * d * d * a.n
-    return {
-        "metric": "OPQ32 encode vectors/sec + ADC queries/sec @ recall@10, 1M×1536 fp32 (BASELINE configs[2])",
-        "value": a.n / wall, "unit": "vectors/s", "ms_per_step": wall * 1e3, "dtype": "f32",
-        "config": {"workload": f"opq32_encode_{a.n}x{d}", "M": M, "nbits": 8, "opq_outer_iters": a.opq_iters},
-        "roofline": {"bound": "mfma", "kernel": "mivq_opq_rotate (rocBLAS fp32 sgemm)", "achieved": flops / (rot_ms * 1e-3) / 1e12,
-                     "peak": MFMA_F32_PEAK_TFS, "unit": "TFLOP/s", "frac": flops / (rot_ms * 1e-3) / 1e12 / MFMA_F32_PEAK_TFS,
-                     "rotate_ms": rot_ms, "encode_call_ms": dev_ms - rot_ms},
-        "adc": {"qps": a.nq / swall, "nq": a.nq, "k": 10, "recall@10": rec, "recall_queries": 100,
-                "ms_per_batch": swall * 1e3},
-    }
-
-
-def run_flatcodes(a, dev, kind):
-    d = 3072
-    g = torch.Generator(device=dev)
-    g.manual_seed(2)
-    X = torch.randn((a.n, d), generator=g, device=dev, dtype=torch.float32)
-    if kind == "sq8":
-        lo = X.amin(0)
-        hi = X.amax(0)
-        den = (hi - lo) + 1e-8
-        enc = lambda: _native.sq_encode(X, lo, den, 8)  # noqa: E731
-        dec = lambda c: _native.sq_decode(c, d, lo, den, 8)  # noqa: E731
-        bytes_per = 4 * d + d
-    else:
-        enc = lambda: _native.rabitq_encode(X, None, _native.METRIC_L2)  # noqa: E731
-        dec = lambda c: _native.rabitq_decode(c, d, None)  # noqa: E731
-        bytes_per = 4 * d + d // 8 + 8
-    wall, dev_ms = timed(enc, a.steps, a.warmup)
-    codes = enc()
-    Q = X[:100].contiguous()  # reference convention: queries = first rows of the database
-
-    def search():
-        return _native.flat_search(Q, dec(codes), 10)
-
-    swall, _ = timed(search, 2, 1)
-    _, ai = search()
-    _, gi = _native.flat_search(Q, X, 10)
-    rec = recall(gi.cpu().numpy(), ai.cpu().numpy(), 10)
-    ach = a.n * bytes_per / (dev_ms * 1e-3) / 1e9
-    est = None
-    if kind == "rabitq1":  # RaBitQIndex: IndexRaBitQ estimator search (center = mean, qb = 4)
-        center = X.double().mean(0).float().contiguous()
-        codes_c = _native.rabitq_encode(X, center, _native.METRIC_L2)
-        Qe = X[: a.nq].contiguous()
-
-        def est_search():
-            return _native.rabitq_search(codes_c, d, center, Qe, 4, _native.METRIC_L2, 10)
-
-        ewall, edev = timed(est_search, 3, 1)
-        _, ei = est_search()
-        est = {"qps": a.nq / ewall, "nq": a.nq, "k": 10, "qb": 4, "ms_per_batch": ewall * 1e3,
-               "recall@10": recall(gi.cpu().numpy(), ei[:100].cpu().numpy(), 10),
-               "codes_bytes": int(codes_c.numel()),
-               "method": "mivq_rabitq_search: int8 MFMA over sign bits + estimator + tiled top-k"}
-    return {
-        "metric": f"{kind} encode vectors/sec + search queries/sec @ recall@10, 1M×3072 fp32 (BASELINE configs[3])",
-        "value": a.n / wall, "unit": "vectors/s", "ms_per_step": wall * 1e3, "dtype": "f32",
-        "config": {"workload": f"{kind}_encode_{a.n}x{d}"},
-        "roofline": {"bound": "hbm", "kernel": f"{kind}_encode", "achieved": ach, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                     "frac": ach / HBM_PEAK_GBS, "bytes_per_vector": bytes_per, "kernel_ms": dev_ms},
-        "search": {"qps": 100 / swall, "nq": 100, "k": 10, "recall@10": rec,
-                   "method": "decode + exact L2 scan of the reconstructions (reference flat search)"},
-        "estimator_search": est,
-    }
 
 
 def run_ivfpq(a, dev):
@@ -208,14 +104,15 @@ def main():
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--opq-iters", type=int, default=10)
+    ap.add_argument("--data", choices=("gaussian", "clustered"), default="clustered")
     a = ap.parse_args()
     dev = _native.require_device()
     if a.workload == "opq32":
-        out = run_opq32(a, dev)
+        out = opq32_leg(a, dev, a.steps, a.warmup)
     elif a.workload == "ivfpq":
         out = run_ivfpq(a, dev)
     else:
-        out = run_flatcodes(a, dev, a.workload)
+        out = flatcodes_leg(a, dev, a.workload, a.steps, a.warmup)
     out.update({"n_gpus": 1, "steps": a.steps, "warmup": a.warmup, "higher_is_better": True, "data": "synthetic"})
     print(json.dumps(out), flush=True)
 

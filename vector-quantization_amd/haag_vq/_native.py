@@ -268,6 +268,11 @@ def opq_rotate(x: torch.Tensor, A: torch.Tensor, transpose: bool = False,
     return out
 
 
+def opq_backend() -> str:
+    """What mivq_opq_rotate runs (for reports)."""
+    return "rocBLAS sgemm"
+
+
 # ----------------------------------------------------------------- SQ
 def sq_encode(x: torch.Tensor, lo: torch.Tensor, den: torch.Tensor, nbits: int) -> torch.Tensor:
     if x.dtype not in (torch.float32, torch.float64):

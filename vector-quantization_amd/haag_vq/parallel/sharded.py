@@ -11,15 +11,14 @@ One process per GPU (torch.distributed, backend "nccl" = RCCL over xGMI):
   1, 2, 4 or 8 GPUs.
 
 The exchange is written against the ``torch.distributed`` API only, so the same code runs
-over gloo on CPU tensors in the multi-process tests (tests/test_sharded_cpu.py).
+over gloo on CPU tensors in the multi-process tests (tests/test_host_cpu.py::
+test_exchange_topk_gloo_world2_matches_single_rank, tests/test_bench_launcher.py).
 """
 
 from __future__ import annotations
 
-import time
 from typing import Callable, Optional, Tuple
 
-import numpy as np
 import torch
 import torch.distributed as dist
 
@@ -73,34 +72,3 @@ def sharded_exact_search(Q: torch.Tensor, X: torch.Tensor, k: int, id_offset: in
                          metric: int = _native.METRIC_L2) -> Tuple[torch.Tensor, torch.Tensor]:
     d, i = _native.flat_search(Q, X, k, metric, id_offset=id_offset)
     return exchange_topk(d, i, k)
-
-
-def bench_adc(X: torch.Tensor, C: torch.Tensor, codes: torch.Tensor, nbits: int, rank: int, world: int,
-              dev: torch.device, Q: torch.Tensor, k: int = 10, gt_queries: int = 100, reps: int = 3) -> dict:
-    """ADC queries/s and recall@k of the sharded index (bench.py's second leg)."""
-    n, d = X.shape
-    nq = Q.shape[0]
-    broadcast_(Q)
-    off = rank * n
-    u8 = codes if nbits == 8 else _native.pq_unpack(codes, C.shape[0], nbits)
-    sharded_adc_search(Q, C, u8, nbits, k, off)  # warm-up
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    t0 = time.perf_counter()
-    for _ in range(reps):
-        ad, ai = sharded_adc_search(Q, C, u8, nbits, k, off)
-    torch.cuda.synchronize()
-    dt = (time.perf_counter() - t0) / reps
-    if world > 1:
-        t = torch.tensor([dt], device=dev, dtype=torch.float64)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        dt = float(t.item())
-    gq = min(gt_queries, nq)
-    _, gi = sharded_exact_search(Q[:gq].contiguous(), X, k, off)
-    got = ai[:gq].cpu().numpy().view(np.uint32)
-    gt = gi.cpu().numpy().view(np.uint32)
-    rec = float(np.mean([len(set(gt[j]) & set(got[j])) / k for j in range(gq)]))
-    return {"qps": nq / dt, "nq": nq, "k": k, "n_total": n * world, f"recall@{k}": rec,
-            "recall_queries": gq, "ms_per_batch": dt * 1e3,
-            "gt": "exact L2 top-k over the raw vectors (mivq_flat_search, sharded + merged)"}

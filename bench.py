@@ -54,6 +54,7 @@ from haag_vq.parallel import sharded  # noqa: E402
 METRIC = "PQ-encode vectors/sec + ADC queries/sec @ recall@10, 1M×1536 fp32"
 HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md chip table (spec)
 MFMA_F32_PEAK_TFS = 157.3      # dense fp32 matrix peak (same table)
+MFMA_F16_PEAK_TFS = 2516.6     # dense f16/bf16 matrix peak = 16 x fp32 (same table)
 LDS_PEAK_GBS = 256 * 256 * 2.4  # 256 CUs x 256 B/clk (ds_read_b128) x 2.4 GHz = 157 TB/s
 # rigorous relative bound on a canonical fp32 score difference (oracle header): 2 (2 g_96 + u)
 CLEAR_GAP = 3e-5
@@ -312,12 +313,11 @@ def opq32_leg(a, dev, steps, warmup):
     opq.fit(X[:65536])
     torch.cuda.synchronize()
     t_fit = time.perf_counter() - t0
-    A = opq.opq.A_device
     C = opq.inner.centroids_device
     prep = _native.pq_prepare(C, 8)
     Y = torch.empty_like(X)
     codes = torch.empty((n, M), dtype=torch.uint8, device=dev)
-    rot = lambda: _native.opq_rotate(X, A, False, out=Y)  # noqa: E731
+    rot = lambda: opq.opq.rotate(X, False, out=Y)  # noqa: E731
 
     def step():
         rot()
@@ -328,25 +328,31 @@ def opq32_leg(a, dev, steps, warmup):
     Q = X[:a.nq].contiguous()  # the reference's convention: queries are the first rows
 
     def search():
-        lut = _native.adc_lut(_native.opq_rotate(Q, A, False), C, 8)
+        lut = _native.adc_lut(opq.opq.rotate(Q, False), C, 8)
         return _native.adc_search(lut, codes, 10, 8)
 
     swall, _ = timed(search, 3, 1)
     _, ai = search()
     _, gi = _native.flat_search(Q[:100].contiguous(), X, 10)
-    Xhat = _native.opq_rotate(_native.pq_decode(codes, C, 8), A, True)
+    Xhat = opq.opq.rotate(_native.pq_decode(codes, C, 8), True)
     _, di = _native.flat_search(Q[:100].contiguous(), Xhat, 10)
     del Xhat, X, Y
     g, r, dd = (t.cpu().numpy() for t in (gi, ai[:100], di))
     rec = lambda ref, x: float(np.mean([len(set(ref[j]) & set(x[j])) / 10 for j in range(len(ref))]))  # noqa: E731
-    flops = 2.0 * d * d * n
+    flops = 2.0 * d * d * n  # the fp32 GEMM's flops (algorithmic)
     tfs = flops / (rot_ms * 1e-3) / 1e12
+    split = _native.opq_prepare(opq.opq.A_device) is not None
+    # the split-f16 kernel spends 3 f16 MFMAs per fp32-accurate multiply-add: its ceiling is
+    # the dense f16 peak / 3; the plain fp32 MFMA kernel's is the fp32 matrix peak
+    peak = MFMA_F16_PEAK_TFS / 3 if split else MFMA_F32_PEAK_TFS
     return {"metric": "OPQ32 encode vectors/sec + ADC queries/sec @ recall@10, 1M×1536 fp32 (BASELINE configs[2])",
             "value": n / wall, "unit": "vectors/s", "ms_per_step": wall * 1e3, "dtype": "f32",
             "config": {"workload": f"opq32_encode_{n}x{d}", "M": M, "nbits": 8, "opq_outer_iters": a.opq_iters,
                        "fit_s": t_fit, "data": a.data},
-            "roofline": {"bound": "mfma", "kernel": f"mivq_opq_rotate ({_native.opq_backend()})", "achieved": tfs,
-                         "peak": MFMA_F32_PEAK_TFS, "unit": "TFLOP/s", "frac": tfs / MFMA_F32_PEAK_TFS,
+            "roofline": {"bound": "mfma", "kernel": _native.opq_backend() if split else "opq_gemm_kernel (fp32 MFMA)",
+                         "achieved": tfs, "peak": peak, "unit": "TFLOP/s (fp32-accurate)", "frac": tfs / peak,
+                         "peak_note": "dense f16 MFMA peak / 3 (x_hi b_hi + x_hi b_lo + x_lo b_hi)" if split else
+                                      "dense fp32 MFMA peak", "vs_fp32_mfma_peak": tfs / MFMA_F32_PEAK_TFS,
                          "rotate_ms": rot_ms, "encode_call_ms": dev_ms - rot_ms},
             "adc": {"qps": a.nq / swall, "nq": a.nq, "k": 10, "recall@10": rec(g, r), "recall_queries": 100,
                     "recall@10_decode_exact": rec(g, dd), "topk_agreement_adc_vs_decode_exact": rec(dd, r),

@@ -105,6 +105,17 @@ int mivq_kmeans_update(const float* x, int64_t n, int32_t d, int32_t M, int32_t 
 int mivq_opq_rotate(const float* x, int64_t n, int32_t d, const float* A, int32_t transpose,
                     float* y, void* stream);
 
+/* The same rotation at f16-MFMA speed with fp32 accuracy (the product path of
+ * OptimizedProductQuantizer): mivq_opq_prepare splits op(A) once into scaled f16 hi / lo
+ * images (prep: mivq_opq_prep_bytes(d) bytes, 16-byte aligned; 0 when d % 8 != 0), and
+ * mivq_opq_rotate_prepared computes y = x . op(A) as x_hi b_hi + x_hi b_lo + x_lo b_hi with
+ * per-row power-of-two scales of x (workspace: mivq_opq_rotate_workspace_bytes). */
+size_t mivq_opq_prep_bytes(int32_t d);
+int mivq_opq_prepare(const float* A, int32_t d, int32_t transpose, void* prep, void* stream);
+size_t mivq_opq_rotate_workspace_bytes(int64_t n, int32_t d);
+int mivq_opq_rotate_prepared(const float* x, int64_t n, int32_t d, const void* prep, void* workspace,
+                             size_t workspace_bytes, float* y, void* stream);
+
 /* ------------------------------------------------------ scalar quantizer
  * Replaces ScalarQuantizer._compress_block / decompress (scalar_quantization.py:52-90)
  * bit-for-bit, in the dtype numpy would compute in (f32 input -> f32 math, f64 -> f64).

@@ -1,0 +1,113 @@
+"""OPQ on the GPU: the hand-written rotation kernels against fp64 and against each other,
+one step of the alternating optimisation against a numpy restatement, and OPQ codes against
+the canonical encode of the rotated vectors (SURVEY.md §8a row a4, §8c "OPQ bit-exactness":
+codes identical to the canonical encode of the GPU-rotated x, rotated values within 1e-5
+relative)."""
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+torch = pytest.importorskip("torch")
+
+# |y - y64| <= TOL * ||x_row|| * ||a_col||: the fp32 rounding budget of a d-term dot product
+TOL = 1e-5
+
+
+def _t(a, dev):
+    return torch.from_numpy(np.ascontiguousarray(a)).to(dev)
+
+
+def _orth(d, seed):
+    q, _ = np.linalg.qr(np.random.default_rng(seed).standard_normal((d, d)))
+    return q.astype(np.float32)
+
+
+def _check(y, X, B):
+    """y vs fp64 X @ B, relative to ||x_i|| ||b_j|| (NaN / inf rows must stay non-finite)."""
+    ref = X.astype(np.float64) @ B.astype(np.float64)
+    fin = np.isfinite(X).all(1)
+    scale = np.linalg.norm(X[fin].astype(np.float64), axis=1)[:, None] * np.linalg.norm(B, axis=0)[None, :]
+    err = np.abs(y[fin] - ref[fin])
+    ok = err <= TOL * scale + 1e-30
+    assert ok.all(), f"max rel err {np.max(err / np.maximum(scale, 1e-300)):.3e}"
+    assert not np.isfinite(y[~fin]).all(axis=1).any()
+
+
+@pytest.mark.parametrize("n,d", [(1000, 1536), (777, 1024), (300, 776), (65, 8), (1, 64)])
+@pytest.mark.parametrize("transpose", [False, True])
+def test_split_gemm_vs_fp64(dev, n, d, transpose):
+    from haag_vq import _native
+
+    rng = np.random.default_rng(n + d)
+    X = rng.standard_normal((n, d)).astype(np.float32)
+    if n > 10:
+        X[3] *= 1e-20          # tiny row (per-row scale)
+        X[4] *= 1e20           # huge row
+        X[5] = 0.0
+        X[6, 1] = np.nan
+        X[7, 2] = np.inf
+        X[8, ::3] *= 1e-6      # mixed magnitudes inside a row
+    A = _orth(d, d) * (3.0 if d == 1024 else 1.0)  # also a non-orthonormal scale
+    prep = _native.opq_prepare(_t(A, dev), transpose)
+    assert prep is not None
+    y = _native.opq_rotate_prepared(_t(X, dev), prep).cpu().numpy()
+    _check(y, X, A if transpose else A.T)
+
+
+@pytest.mark.parametrize("n,d", [(500, 1536), (130, 100)])
+def test_fp32_mfma_kernel_vs_fp64(dev, n, d):
+    """mivq_opq_rotate: the plain fp32 MFMA kernel (any d, no preparation)."""
+    from haag_vq import _native
+
+    X = np.random.default_rng(1).standard_normal((n, d)).astype(np.float32)
+    A = _orth(d, 2)
+    for tr in (False, True):
+        y = _native.opq_rotate(_t(X, dev), _t(A, dev), tr).cpu().numpy()
+        _check(y, X, A if tr else A.T)
+
+
+def test_prepare_rejects_d_not_multiple_of_8(dev):
+    from haag_vq import _native
+
+    assert _native.opq_prepare(_t(_orth(100, 0), dev)) is None
+
+
+def test_opq_train_step_matches_restatement(dev, oracle):
+    """One alternating-optimisation round (optimized_product_quantization.py:21-28 via faiss
+    OPQMatrix::train): GPU vs numpy given the round's trained codebook."""
+    from haag_vq.methods.optimized_product_quantization import OptimizedProductQuantizer
+
+    rng = np.random.default_rng(4)
+    X = (rng.standard_normal((3000, 64)) @ rng.standard_normal((64, 64))).astype(np.float32)
+    opq = OptimizedProductQuantizer(M=8, B=8)
+    Xd = _t(X, dev)
+    A0 = opq.initial_rotation(64, dev)
+    A1, C, Y, Yhat = opq.train_step(Xd, A0, None, 0)
+    A0h, Yh, Ch = A0.cpu().numpy(), Y.cpu().numpy(), C.cpu().numpy()
+    _check(Yh, X, A0h.T)                                                  # rotate
+    codes = oracle.pq_encode(Yh, Ch)                                      # canonical encode
+    np.testing.assert_array_equal(Yhat.cpu().numpy(), oracle.pq_decode(codes, Ch))  # bit-exact decode
+    G = X.astype(np.float64).T @ oracle.pq_decode(codes, Ch).astype(np.float64)
+    U, _, Vt = np.linalg.svd(G)
+    np.testing.assert_allclose(A1.cpu().numpy(), (Vt.T @ U.T), atol=2e-6)  # Procrustes
+    A1h = A1.cpu().numpy().astype(np.float64)
+    np.testing.assert_allclose(A1h @ A1h.T, np.eye(64), atol=1e-5)
+
+
+def test_opq_codes_are_canonical_encode_of_rotated(dev, oracle):
+    from haag_vq.methods.optimized_product_quantization import OptimizedProductQuantizer
+
+    rng = np.random.default_rng(5)
+    X = rng.standard_normal((4000, 256)).astype(np.float32)
+    opq = OptimizedProductQuantizer(M=16, B=8)
+    opq.niter = 3
+    opq.fit(X)
+    codes = opq.compress(X)
+    Y = opq.opq.apply(X)                       # the GPU-rotated vectors
+    C = np.stack(opq.inner.codebooks).astype(np.float32)
+    np.testing.assert_array_equal(codes, oracle.pq_encode(Y, C))
+    _check(Y, X, opq.opq.A.reshape(256, 256).T)
+    rec = opq.decompress(codes)
+    _check(rec, oracle.pq_decode(codes, C), opq.opq.A.reshape(256, 256))

@@ -1,25 +1,37 @@
-// opq.hip — OPQ rotation as an fp32 MFMA GEMM on gfx950.
+// opq.hip — OPQ rotation y = x . op(A) as a hand-written MFMA GEMM on gfx950.
 //
 // Replaces faiss.OPQMatrix.apply / reverse_transform used by OptimizedProductQuantizer
 // (/root/reference/src/haag_vq/methods/optimized_product_quantization.py:26,31,34):
 //   transpose == 0 : y = x . A^T   (LinearTransform::apply, A is d_out x d_in row-major)
 //   transpose == 1 : y = x . A     (reverse_transform of an orthonormal A)
-// The rotation is a genuine dense contraction, so it runs on the matrix cores in exact
-// f32 (v_mfma_f32_32x32x2_f32: each instruction is a k-ordered fmaf chain, no reduced
-// precision).  128x128 output tile per 256-thread workgroup, 2x2 32x32 tiles per wave,
-// BK = 16 slices of x and A staged through LDS (k-major so every fragment read is a
-// contiguous, conflict-free 128-B row).
 //
-// mivq_opq_rotate itself runs the library fp32 GEMM (rocBLAS sgemm on the caller's stream,
-// 147 TFLOP/s at 1M x 1536 against 56 for opq_gemm_kernel — tools/dbg/gemm_probe.py): the
-// rotation is a plain GEMM with nothing to fuse.  MIVQ_OPQ_NATIVE_GEMM=1 selects the kernel
-// below instead; it also serves when rocBLAS reports an error.
-#include <rocblas/rocblas.h>
+// Two kernels:
+//
+// 1. opq_split_gemm_kernel (mivq_opq_rotate_prepared, the product path): fp32-accurate
+//    GEMM out of f16 MFMAs.  Every operand is split into two f16 terms, v = hi + lo with
+//    hi = f16(s v), lo = f16(s v - hi) (the difference is exact in fp32), after a
+//    power-of-two scale s that puts the largest |v| of the row (x) or of the matrix (A) at
+//    2^13..2^14, inside f16's range.  y = (x_hi b_hi + x_hi b_lo + x_lo b_hi) / (s_x s_b):
+//    each f16 x f16 product is exact in the fp32 accumulator, and the terms left out
+//    (x_lo b_lo and the residuals of the two splits) are <= ~3 * 2^-22 of |x_k b_k|, far
+//    below the fp32 accumulation rounding every GEMM has (tests/test_opq_gpu.py checks
+//    1e-5 of ||x|| ||a|| against fp64).  Three v_mfma_f32_32x32x16_f16 per 32x32x16 block
+//    = 3 x 1/16 of the fp32-MFMA cost per flop (2.5 PF f16 vs 157 TF fp32 dense peaks).
+//    Tile: 128 x 128 outputs per 256-thread workgroup, 64 x 64 (2 x 2 MFMA blocks) per
+//    wave, K in steps of 32 staged through LDS (hi and lo planes of x and B, 80-B rows:
+//    conflict-free ds_read_b128 fragment reads), double-buffered with the next step's
+//    global loads in registers while the current step computes.  XCD-aware tile order:
+//    the workgroups one XCD runs cover consecutive tiles, so the column tiles of one row
+//    block run back to back on the same L2 (x read once from HBM).
+//    mivq_opq_prepare builds the hi / lo images of B = op(A) once per matrix ([col][k]
+//    rows, scaled); mivq_opq_rotate_prepared computes the row scales of x (one pass) and
+//    runs the GEMM.
+//
+// 2. opq_gemm_kernel (mivq_opq_rotate, no preparation, any d): plain fp32 MFMA
+//    (v_mfma_f32_32x32x2_f32), 128 x 128 tiles, BK = 16 slices staged through LDS.
+#include <math.h>
 
 #include <algorithm>
-#include <cstdlib>
-#include <map>
-#include <mutex>
 
 #include "mivq_common.h"
 
@@ -27,7 +39,10 @@ namespace mivq {
 namespace {
 
 typedef float floatx16 __attribute__((ext_vector_type(16)));
+typedef _Float16 half8 __attribute__((ext_vector_type(8)));
+typedef _Float16 half4 __attribute__((ext_vector_type(4)));
 
+// ------------------------------------------------------------------ fp32 MFMA kernel
 constexpr int BM = 128, BN = 128, BK = 16, PAD = 4;
 
 __global__ __launch_bounds__(256) void opq_gemm_kernel(const float* __restrict__ x, int64_t n, int d,
@@ -49,7 +64,6 @@ __global__ __launch_bounds__(256) void opq_gemm_kernel(const float* __restrict__
 
     const int kl = lane >> 5, il = lane & 31;
     for (int k0 = 0; k0 < d; k0 += BK) {
-        // x tile: 128 rows x 16 k = 2048 floats, 8 per thread
 #pragma unroll
         for (int q = 0; q < 8; ++q) {
             const int e = tid + q * 256;
@@ -57,7 +71,6 @@ __global__ __launch_bounds__(256) void opq_gemm_kernel(const float* __restrict__
             const int64_t row = r0 + i;
             xs[kk][i] = (row < n && k0 + kk < d) ? x[row * d + k0 + kk] : 0.0f;
         }
-        // B tile: 16 k x 128 cols
 #pragma unroll
         for (int q = 0; q < 8; ++q) {
             const int e = tid + q * 256;
@@ -97,47 +110,228 @@ __global__ __launch_bounds__(256) void opq_gemm_kernel(const float* __restrict__
             }
 }
 
-}  // namespace
-}  // namespace mivq
+// ------------------------------------------------------------------ split-f16 kernel
+constexpr int SBM = 128, SBN = 128, SBK = 32;
+constexpr int SPITCH = SBK * 2 + 16;          // bytes per LDS row (64 B of halves + 16 B pad)
+constexpr int SPLANE = 128 * SPITCH;          // one 128-row plane (hi or lo of x or of B)
+constexpr int SBUF = 4 * SPLANE;              // x hi, x lo, B hi, B lo
+constexpr int kSplitSmem = 2 * SBUF;          // double-buffered: 80 KiB
+constexpr int kScaleShift = 14;               // largest |v| scaled into [2^13, 2^14]
 
-namespace mivq {
-namespace {
-
-// One rocBLAS handle per device, created on first use and kept for the process.
-rocblas_handle blas_handle() {
-    static std::mutex mu;
-    static std::map<int, rocblas_handle> handles;
-    int dev = 0;
-    if (hipGetDevice(&dev) != hipSuccess) return nullptr;
-    std::lock_guard<std::mutex> lk(mu);
-    auto it = handles.find(dev);
-    if (it != handles.end()) return it->second;
-    rocblas_handle h = nullptr;
-    if (rocblas_create_handle(&h) != rocblas_status_success) return nullptr;
-    handles[dev] = h;
-    return h;
+// Power-of-two scale 2^(14 - E) with max|v| = m 2^E, m in [0.5, 1); 1 for 0 / inf / NaN.
+// Clamped to fp32's normal exponents (rows below 2^-112 lose relative accuracy).
+__device__ __forceinline__ float pow2_scale(float amax) {
+    if (!(amax > 0.0f) || !isfinite(amax)) return 1.0f;
+    int e;
+    (void)frexpf(amax, &e);
+    const int sh = min(126, max(-126, kScaleShift - e));
+    return ldexpf(1.0f, sh);
 }
 
-// y (n x d, row-major) = x . A^T (transpose 0) or x . A (transpose 1).  Column-major view:
-// Y^T = op(A_cm) . X^T with A_cm = A^T as stored, so op = T for x . A^T and N for x . A.
-bool rotate_blas(const float* x, int64_t n, int d, const float* A, int transpose, float* y, hipStream_t st) {
-    static const bool native = [] {
-        const char* e = std::getenv("MIVQ_OPQ_NATIVE_GEMM");
-        return e && e[0] == '1';
-    }();
-    if (native) return false;
-    rocblas_handle h = blas_handle();
-    if (!h || rocblas_set_stream(h, st) != rocblas_status_success) return false;
-    const float one = 1.0f, zero = 0.0f;
-    const int64_t step = (int64_t)1 << 30;  // rocblas_int columns per call
-    for (int64_t r = 0; r < n; r += step) {
-        const int cols = (int)std::min<int64_t>(step, n - r);
-        if (rocblas_sgemm(h, transpose ? rocblas_operation_none : rocblas_operation_transpose, rocblas_operation_none,
-                          d, cols, d, &one, A, d, x + r * d, d, &zero, y + r * d, d) != rocblas_status_success)
-            return false;
+__device__ __forceinline__ void split2(float v, _Float16& hi, _Float16& lo) {
+    hi = (_Float16)v;
+    lo = (_Float16)(v - (float)hi);
+}
+
+// Per-row scale of x: one wave per row.
+__global__ __launch_bounds__(256) void opq_row_scale_kernel(const float* __restrict__ x, int64_t n, int d,
+                                                            float* __restrict__ rs) {
+    const int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    const int l = threadIdx.x & 63;
+    if (row >= n) return;
+    const float* xr = x + row * d;
+    float m = 0.0f;
+    bool bad = false;
+    for (int k = l; k < d; k += 64) {
+        const float v = xr[k];
+        bad |= !isfinite(v);
+        m = fmaxf(m, fabsf(v));
     }
-    return true;
+    for (int o = 32; o > 0; o >>= 1) m = fmaxf(m, __shfl_xor(m, o));
+    bad = __any(bad);
+    if (l == 0) rs[row] = bad ? 1.0f : pow2_scale(m);
 }
+
+// max |A| over the whole matrix -> header {s_b, 1 / s_b} of the prepared image (one workgroup).
+__global__ __launch_bounds__(1024) void opq_absmax_kernel(const float* __restrict__ A, int64_t cnt,
+                                                          float* __restrict__ hdr) {
+    __shared__ float red[16];
+    __shared__ int bad_any;
+    if (threadIdx.x == 0) bad_any = 0;
+    __syncthreads();
+    float m = 0.0f;
+    bool bad = false;
+    for (int64_t i = threadIdx.x; i < cnt; i += 1024) {
+        const float v = A[i];
+        bad |= !isfinite(v);
+        m = fmaxf(m, fabsf(v));
+    }
+    for (int o = 32; o > 0; o >>= 1) m = fmaxf(m, __shfl_xor(m, o));
+    if (__any(bad) && (threadIdx.x & 63) == 0) atomicOr(&bad_any, 1);
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = m;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        float mm = 0.0f;
+        for (int i = 0; i < 16; ++i) mm = fmaxf(mm, red[i]);
+        const float s = bad_any ? 1.0f : pow2_scale(mm);
+        hdr[0] = s;
+        hdr[1] = 1.0f / s;
+    }
+}
+
+// B image: bimg[plane][j][k] = split(s_b * op(A)[k][j]), plane 0 = hi, 1 = lo; op(A)[k][j] =
+// A[j][k] for transpose 0 (y = x A^T), A[k][j] for transpose 1.
+__global__ __launch_bounds__(256) void opq_split_b_kernel(const float* __restrict__ A, int d, int transpose,
+                                                          const float* __restrict__ hdr, _Float16* __restrict__ bimg) {
+    const int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    const int64_t dd = (int64_t)d * d;
+    if (e >= dd) return;
+    const int j = (int)(e / d), k = (int)(e - (int64_t)j * d);
+    const float v = (transpose == 0 ? A[(int64_t)j * d + k] : A[(int64_t)k * d + j]) * hdr[0];
+    _Float16 hi, lo;
+    split2(v, hi, lo);
+    bimg[e] = hi;
+    bimg[dd + e] = lo;
+}
+
+// Tile t of workgroup b: the workgroups of one XCD (b % 8, dealt round-robin) take a
+// contiguous range of tiles, so consecutive tiles (the column tiles of one row block) share
+// that XCD's L2.
+__device__ __forceinline__ int64_t xcd_tile(int64_t b, int64_t G) {
+    const int64_t x = b & 7, j = b >> 3, q = G >> 3, r = G & 7;
+    return x * q + min(x, r) + j;
+}
+
+__global__ __launch_bounds__(256) void opq_split_gemm_kernel(const float* __restrict__ x, int64_t n, int d,
+                                                             const float* __restrict__ rs,
+                                                             const _Float16* __restrict__ bimg,
+                                                             const float* __restrict__ hdr, float* __restrict__ y,
+                                                             int64_t ctiles) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    const int tid = threadIdx.x, l = tid & 63, w = tid >> 6;
+    const int wr = w >> 1, wc = w & 1;
+    const int64_t t = xcd_tile(blockIdx.x, gridDim.x);
+    const int64_t r0 = (t / ctiles) * SBM;
+    const int c0 = (int)(t % ctiles) * SBN;
+    const int64_t dd = (int64_t)d * d;
+
+    // staging geometry: x: 4 float4 per thread (row e / 8, k 4 (e % 8)); B: 4 x 16 B per
+    // thread (plane e / 512, col (e % 512) / 4, k 8 (e % 4))
+    float sx[4];
+    int xrow[4], xk[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+        const int e = tid + 256 * u;
+        xrow[u] = e >> 3;
+        xk[u] = 4 * (e & 7);
+        const int64_t gr = r0 + xrow[u];
+        sx[u] = gr < n ? rs[gr] : 0.0f;
+    }
+    int bpl[4], bcol[4], bk[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+        const int e = tid + 256 * u;
+        bpl[u] = e >> 9;
+        bcol[u] = (e & 511) >> 2;
+        bk[u] = 8 * (e & 3);
+    }
+    float4 xv[4];
+    uint4 bv[4];
+    auto gload = [&](int k0) __attribute__((always_inline)) {
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            const int64_t gr = r0 + xrow[u];
+            const int k = k0 + xk[u];
+            xv[u] = (gr < n && k < d) ? *reinterpret_cast<const float4*>(x + gr * d + k) : make_float4(0.f, 0.f, 0.f, 0.f);
+            const int gc = c0 + bcol[u], kb = k0 + bk[u];
+            bv[u] = (gc < d && kb < d) ? *reinterpret_cast<const uint4*>(bimg + bpl[u] * dd + (int64_t)gc * d + kb)
+                                       : make_uint4(0u, 0u, 0u, 0u);
+        }
+    };
+    auto sstore = [&](unsigned char* buf) __attribute__((always_inline)) {
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            half4 h, lo;
+            const float v[4] = {xv[u].x * sx[u], xv[u].y * sx[u], xv[u].z * sx[u], xv[u].w * sx[u]};
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                _Float16 a, b;
+                split2(v[q], a, b);
+                h[q] = a;
+                lo[q] = b;
+            }
+            const int off = xrow[u] * SPITCH + 2 * xk[u];
+            *reinterpret_cast<half4*>(buf + off) = h;
+            *reinterpret_cast<half4*>(buf + SPLANE + off) = lo;
+            *reinterpret_cast<uint4*>(buf + (2 + bpl[u]) * SPLANE + bcol[u] * SPITCH + 2 * bk[u]) = bv[u];
+        }
+    };
+
+    floatx16 acc[2][2];
+#pragma unroll
+    for (int a = 0; a < 2; ++a)
+#pragma unroll
+        for (int b = 0; b < 2; ++b)
+#pragma unroll
+            for (int e = 0; e < 16; ++e) acc[a][b][e] = 0.0f;
+
+    const int nsteps = (d + SBK - 1) / SBK;
+    gload(0);
+    sstore(smem);
+    __syncthreads();
+    const int fr = l & 31, fk = 16 * (l >> 5);  // fragment row / col and byte offset of its k-group
+    for (int s = 0; s < nsteps; ++s) {
+        unsigned char* cur = smem + (s & 1) * SBUF;
+        if (s + 1 < nsteps) gload((s + 1) * SBK);
+#pragma unroll
+        for (int kk = 0; kk < 2; ++kk) {
+            half8 ah[2], al[2], bh[2], bl[2];
+#pragma unroll
+            for (int i = 0; i < 2; ++i) {
+                const int ar = (wr * 64 + i * 32 + fr) * SPITCH + 32 * kk + fk;
+                const int bc = (wc * 64 + i * 32 + fr) * SPITCH + 32 * kk + fk;
+                ah[i] = *reinterpret_cast<const half8*>(cur + ar);
+                al[i] = *reinterpret_cast<const half8*>(cur + SPLANE + ar);
+                bh[i] = *reinterpret_cast<const half8*>(cur + 2 * SPLANE + bc);
+                bl[i] = *reinterpret_cast<const half8*>(cur + 3 * SPLANE + bc);
+            }
+            // small terms first; four independent accumulators between dependent MFMAs
+#pragma unroll
+            for (int a = 0; a < 2; ++a)
+#pragma unroll
+                for (int b = 0; b < 2; ++b) acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x16_f16(al[a], bh[b], acc[a][b], 0, 0, 0);
+#pragma unroll
+            for (int a = 0; a < 2; ++a)
+#pragma unroll
+                for (int b = 0; b < 2; ++b) acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[a], bl[b], acc[a][b], 0, 0, 0);
+#pragma unroll
+            for (int a = 0; a < 2; ++a)
+#pragma unroll
+                for (int b = 0; b < 2; ++b) acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[a], bh[b], acc[a][b], 0, 0, 0);
+        }
+        if (s + 1 < nsteps) sstore(smem + ((s + 1) & 1) * SBUF);
+        __syncthreads();
+    }
+    // epilogue: undo the scales (powers of two: exact) and store
+    const float binv = hdr[1];
+#pragma unroll
+    for (int a = 0; a < 2; ++a) {
+#pragma unroll
+        for (int e = 0; e < 16; ++e) {
+            const int row = wr * 64 + a * 32 + (e & 3) + 8 * (e >> 2) + 4 * (l >> 5);
+            const int64_t gr = r0 + row;
+            if (gr >= n) continue;
+            const float inv = binv / rs[gr];
+#pragma unroll
+            for (int b = 0; b < 2; ++b) {
+                const int gc = c0 + wc * 64 + b * 32 + (l & 31);
+                if (gc < d) y[gr * d + gc] = acc[a][b][e] * inv;
+            }
+        }
+    }
+}
+
+size_t prep_bytes(int32_t d) { return 256 + (size_t)2 * d * d * sizeof(_Float16); }
 
 }  // namespace
 }  // namespace mivq
@@ -150,8 +344,60 @@ extern "C" int mivq_opq_rotate(const float* x, int64_t n, int32_t d, const float
     MIVQ_REQUIRE(transpose == 0 || transpose == 1, MIVQ_ERR_INVALID, "opq_rotate: transpose must be 0 or 1");
     if (n == 0) return MIVQ_OK;
     MIVQ_REQUIRE(x && A && y && x != y, MIVQ_ERR_INVALID, "opq_rotate: null or aliased pointer");
-    if (mivq::rotate_blas(x, n, d, A, transpose, y, as_stream(stream))) return check_launch("opq_rotate (rocBLAS)");
     const dim3 grid((unsigned)ceil_div(n, BM), (unsigned)ceil_div(d, BN));
     hipLaunchKernelGGL(opq_gemm_kernel, grid, dim3(256), 0, as_stream(stream), x, n, d, A, transpose, y);
     return check_launch("opq_rotate");
+}
+
+extern "C" size_t mivq_opq_prep_bytes(int32_t d) { return d > 0 && d % 8 == 0 ? prep_bytes(d) : 0; }
+
+extern "C" int mivq_opq_prepare(const float* A, int32_t d, int32_t transpose, void* prep, void* stream) {
+    MIVQ_REQUIRE(d > 0, MIVQ_ERR_INVALID, "opq_prepare: bad size d=%d", d);
+    MIVQ_REQUIRE(d % 8 == 0, MIVQ_ERR_UNSUPPORTED, "opq_prepare: d=%d must be a multiple of 8 (use mivq_opq_rotate)", d);
+    MIVQ_REQUIRE(transpose == 0 || transpose == 1, MIVQ_ERR_INVALID, "opq_prepare: transpose must be 0 or 1");
+    MIVQ_REQUIRE(A && prep, MIVQ_ERR_INVALID, "opq_prepare: null pointer");
+    hipStream_t st = as_stream(stream);
+    float* hdr = static_cast<float*>(prep);
+    _Float16* bimg = reinterpret_cast<_Float16*>(static_cast<unsigned char*>(prep) + 256);
+    hipLaunchKernelGGL(opq_absmax_kernel, dim3(1), dim3(1024), 0, st, A, (int64_t)d * d, hdr);
+    int rc = check_launch("opq_absmax");
+    if (rc) return rc;
+    hipLaunchKernelGGL(opq_split_b_kernel, dim3((unsigned)ceil_div((int64_t)d * d, 256)), dim3(256), 0, st, A, d,
+                       transpose, hdr, bimg);
+    return check_launch("opq_split_b");
+}
+
+extern "C" size_t mivq_opq_rotate_workspace_bytes(int64_t n, int32_t d) {
+    (void)d;
+    return n > 0 ? align_up((size_t)n * sizeof(float), 256) : 0;
+}
+
+extern "C" int mivq_opq_rotate_prepared(const float* x, int64_t n, int32_t d, const void* prep, void* workspace,
+                                        size_t workspace_bytes, float* y, void* stream) {
+    MIVQ_REQUIRE(n >= 0 && d > 0, MIVQ_ERR_INVALID, "opq_rotate_prepared: bad sizes n=%lld d=%d", (long long)n, d);
+    MIVQ_REQUIRE(d % 8 == 0, MIVQ_ERR_UNSUPPORTED, "opq_rotate_prepared: d=%d must be a multiple of 8", d);
+    if (n == 0) return MIVQ_OK;
+    MIVQ_REQUIRE(x && prep && y && x != y, MIVQ_ERR_INVALID, "opq_rotate_prepared: null or aliased pointer");
+    MIVQ_REQUIRE(reinterpret_cast<uintptr_t>(x) % 16 == 0 && reinterpret_cast<uintptr_t>(prep) % 16 == 0,
+                 MIVQ_ERR_INVALID, "opq_rotate_prepared: x and prep must be 16-byte aligned");
+    const size_t need = mivq_opq_rotate_workspace_bytes(n, d);
+    MIVQ_REQUIRE(workspace && workspace_bytes >= need, MIVQ_ERR_WORKSPACE, "opq_rotate_prepared: workspace %zu < %zu",
+                 workspace_bytes, need);
+    hipStream_t st = as_stream(stream);
+    float* rs = static_cast<float*>(workspace);
+    const float* hdr = static_cast<const float*>(prep);
+    const _Float16* bimg = reinterpret_cast<const _Float16*>(static_cast<const unsigned char*>(prep) + 256);
+    hipLaunchKernelGGL(opq_row_scale_kernel, dim3((unsigned)ceil_div(n, 4)), dim3(256), 0, st, x, n, d, rs);
+    int rc = check_launch("opq_row_scale");
+    if (rc) return rc;
+    static_assert(kSplitSmem <= 160 * 1024, "LDS");
+    hipError_t e = hipFuncSetAttribute((const void*)opq_split_gemm_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                       kSplitSmem);
+    if (e != hipSuccess) return set_error(MIVQ_ERR_HIP, "opq_split_gemm: %s", hipGetErrorString(e));
+    const int64_t ct = ceil_div(d, SBN), tiles = ceil_div(n, SBM) * ct;
+    MIVQ_REQUIRE(tiles < ((int64_t)1 << 31), MIVQ_ERR_UNSUPPORTED, "opq_rotate_prepared: n=%lld too large for one call",
+                 (long long)n);
+    hipLaunchKernelGGL(opq_split_gemm_kernel, dim3((unsigned)tiles), dim3(256), kSplitSmem, st, x, n, d, rs, bimg, hdr,
+                       y, ct);
+    return check_launch("opq_split_gemm");
 }

@@ -1188,10 +1188,15 @@ __global__ __launch_bounds__(256) void pq_transpose_codes16_kernel(const uint8_t
     }
 }
 
+// CU count of the current device, cached per (thread, device): no shared mutable state.
 int device_cus() {
+    constexpr int kMaxDev = 64;
+    static thread_local int cache[kMaxDev] = {};
     int dev = 0, cus = 0;
     if (hipGetDevice(&dev) != hipSuccess) return 256;
+    if (dev >= 0 && dev < kMaxDev && cache[dev] > 0) return cache[dev];
     if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0) return 256;
+    if (dev >= 0 && dev < kMaxDev) cache[dev] = cus;
     return cus;
 }
 
@@ -1244,8 +1249,7 @@ hipError_t launch_pq_encode_cs_v(const float* x, int64_t n, int d, int M, int ds
     auto rkern = pq_resolve_cs_kernel<KS, V>;
     e = hipFuncSetAttribute((const void*)rkern, hipFuncAttributeMaxDynamicSharedMemorySize, rsmem);
     if (e != hipSuccess) return e;
-    static thread_local int cus = 0;
-    if (!cus) cus = device_cus();
+    const int cus = device_cus();
     const int64_t chunks = pick_chunks(n, d, M, cus);
     const int64_t R = align_up(ceil_div(n, chunks), (int64_t)32);
     const int64_t grid = ceil_div(n, R) * M;

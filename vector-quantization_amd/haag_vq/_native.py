@@ -53,6 +53,10 @@ SIGNATURES = {
     "mivq_pq_unpack": (_c.c_int, [_vp, _i64, _i32, _i32, _vp, _vp]),
     "mivq_kmeans_update": (_c.c_int, [_vp, _i64, _i32, _i32, _i32, _vp, _vp, _vp, _vp]),
     "mivq_opq_rotate": (_c.c_int, [_vp, _i64, _i32, _vp, _i32, _vp, _vp]),
+    "mivq_opq_prep_bytes": (_sz, [_i32]),
+    "mivq_opq_prepare": (_c.c_int, [_vp, _i32, _i32, _vp, _vp]),
+    "mivq_opq_rotate_workspace_bytes": (_sz, [_i64, _i32]),
+    "mivq_opq_rotate_prepared": (_c.c_int, [_vp, _i64, _i32, _vp, _vp, _sz, _vp, _vp]),
     "mivq_sq_encode_f32": (_c.c_int, [_vp, _i64, _i32, _vp, _vp, _i32, _vp, _vp]),
     "mivq_sq_encode_f64": (_c.c_int, [_vp, _i64, _i32, _vp, _vp, _i32, _vp, _vp]),
     "mivq_sq_decode_f32": (_c.c_int, [_vp, _i64, _i32, _vp, _vp, _i32, _vp, _vp]),
@@ -269,8 +273,40 @@ def opq_rotate(x: torch.Tensor, A: torch.Tensor, transpose: bool = False,
 
 
 def opq_backend() -> str:
-    """What mivq_opq_rotate runs (for reports)."""
-    return "rocBLAS sgemm"
+    """What the OPQ classes rotate with (for reports)."""
+    return "opq_split_gemm_kernel: split-f16 MFMA GEMM, fp32 accuracy"
+
+
+def opq_prepare(A: torch.Tensor, transpose: bool = False) -> Optional[torch.Tensor]:
+    """Scaled f16 hi / lo image of op(A) for opq_rotate_prepared (None when d % 8 != 0)."""
+    _check(A, "A", torch.float32, 2)
+    d = A.shape[0]
+    if tuple(A.shape) != (d, d):
+        raise ValueError(f"A must be square, got {tuple(A.shape)}")
+    nb = load_library().mivq_opq_prep_bytes(d)
+    if nb == 0:
+        return None
+    prep = torch.empty(nb, dtype=torch.uint8, device=A.device)
+    _call("mivq_opq_prepare", _ptr(A), d, 1 if transpose else 0, _ptr(prep), _stream())
+    return prep
+
+
+def opq_rotate_prepared(x: torch.Tensor, prep: torch.Tensor, out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """y = x . op(A) for the op(A) that `prep` was built from (opq_prepare)."""
+    _check(x, "x", torch.float32, 2)
+    _check(prep, "prep", torch.uint8, 1)
+    n, d = x.shape
+    if prep.numel() != load_library().mivq_opq_prep_bytes(d):
+        raise ValueError(f"prep has {prep.numel()} bytes, not the image of a ({d}, {d}) matrix")
+    if out is None:
+        out = torch.empty_like(x)
+    else:
+        _check(out, "out", torch.float32, 2)
+        if tuple(out.shape) != (n, d):
+            raise ValueError(f"out shape {tuple(out.shape)} != {(n, d)}")
+    ws = workspace(load_library().mivq_opq_rotate_workspace_bytes(n, d), x.device)
+    _call("mivq_opq_rotate_prepared", _ptr(x), n, d, _ptr(prep), _ptr(ws), ws.numel(), _ptr(out), _stream())
+    return out
 
 
 # ----------------------------------------------------------------- SQ
@@ -281,6 +317,8 @@ def sq_encode(x: torch.Tensor, lo: torch.Tensor, den: torch.Tensor, nbits: int) 
     _check(lo, "lo", x.dtype, 1)
     _check(den, "den", x.dtype, 1)
     n, d = x.shape
+    if lo.numel() != d or den.numel() != d:
+        raise ValueError(f"sq_encode: min/max have {lo.numel()}/{den.numel()} entries, data has d={d}")
     if nbits == 16:
         out = torch.empty((n, d), dtype=torch.int16, device=x.device)
     elif nbits == 8:
@@ -301,6 +339,15 @@ def sq_decode(codes: torch.Tensor, d: int, lo: torch.Tensor, den: torch.Tensor, 
     dt = lo.dtype
     _check(lo, "lo", dt, 1)
     _check(den, "den", dt, 1)
+    if lo.numel() != d or den.numel() != d:
+        raise ValueError(f"sq_decode: min/max have {lo.numel()}/{den.numel()} entries, expected d={d}")
+    want = {4: ((d + 1) // 2, (torch.uint8,)), 8: (d, (torch.uint8,)), 16: (d, (torch.int16, torch.uint16))}
+    if nbits not in want:
+        raise ValueError(f"num_bits must be 4, 8, or 16, got {nbits}")
+    width, dtypes = want[nbits]
+    if codes.dim() != 2 or codes.shape[1] != width or codes.dtype not in dtypes:
+        raise ValueError(f"sq_decode: {nbits}-bit codes of d={d} must be ({n}, {width}) {dtypes[0]}, "
+                         f"got {tuple(codes.shape)} {codes.dtype}")
     out = torch.empty((n, d), dtype=dt, device=codes.device)
     fn = "mivq_sq_decode_f64" if dt == torch.float64 else "mivq_sq_decode_f32"
     _call(fn, _ptr(codes), n, d, _ptr(lo), _ptr(den), nbits, _ptr(out), _stream())

@@ -31,10 +31,30 @@ def compute_ground_truth(queries: np.ndarray, vectors: np.ndarray, k: int = 100)
 compute_ground_truth_faiss = compute_ground_truth  # reference name (datasets.py:8)
 
 
+def _default_metric():
+    from sklearn.metrics import pairwise_distances  # the reference's default (datasets.py:43)
+
+    return pairwise_distances
+
+
+def is_euclidean(metric) -> bool:
+    """True for the reference's default ranking metric (sklearn pairwise_distances, Euclidean):
+    its ranking equals the squared-L2 ranking the device kernels compute."""
+    if metric is None:
+        return True
+    try:
+        from sklearn.metrics import pairwise_distances
+    except ImportError:  # pragma: no cover
+        return False
+    return metric is pairwise_distances
+
+
 class Dataset:
     def __init__(self, vectors: np.ndarray, queries: Optional[np.ndarray] = None,
                  ground_truth: Optional[np.ndarray] = None, num_queries: int = 100,
                  distance_metric: Optional[Callable] = None, skip_ground_truth: bool = False):
+        if distance_metric is None:
+            distance_metric = _default_metric()
         self.vectors = vectors
         if queries is None:
             self.queries = vectors[:num_queries]
@@ -72,13 +92,34 @@ def load_local_dataset(path, limit: Optional[int] = None, num_queries: int = 100
     return Dataset(np.ascontiguousarray(X, dtype=np.float32), num_queries=num_queries)
 
 
+# the reference's Hugging Face datasets (sweep.py:121-167) -> local file stems
+_LOCAL_NAMES = {
+    "dbpedia-100k": ("dbpedia-100k", "dbpedia_100k"),
+    "dbpedia-1536": ("dbpedia-1536", "dbpedia_1536"),
+    "dbpedia-3072": ("dbpedia-3072", "dbpedia_3072"),
+    "cohere-msmarco": ("cohere-msmarco", "msmarco"),
+    "huggingface": ("huggingface", "stsb_multi_mt"),
+}
+# upstream's default limits when none is given (sweep.py:131-160)
+_DEFAULT_LIMIT = {"cohere-msmarco": 100_000, "dbpedia-1536": 100_000, "dbpedia-3072": 100_000}
+
+
+def load_named_dataset(name: str, limit: Optional[int] = None, cache_dir: str = "../datasets") -> Dataset:
+    """A dataset the reference downloads, read from $VQ_DATA_DIR (or cache_dir)/<name>.{npy,fvecs}."""
+    if name not in _LOCAL_NAMES:
+        raise ValueError(f"Unsupported dataset: {name}")
+    root = Path(os.environ.get("VQ_DATA_DIR", cache_dir))
+    for stem in _LOCAL_NAMES[name]:
+        for ext in (".npy", ".fvecs"):
+            if (root / f"{stem}{ext}").exists():
+                return load_local_dataset(root / f"{stem}{ext}", limit=limit if limit is not None
+                                          else _DEFAULT_LIMIT.get(name))
+    raise FileNotFoundError(
+        f"{name} is fetched from the Hugging Face Hub by the reference; offline, place "
+        f"{_LOCAL_NAMES[name][0]}.npy or .fvecs under {root} (or set VQ_DATA_DIR)"
+    )
+
+
 def load_dbpedia_openai_1536_100k(limit: Optional[int] = None, cache_dir: str = "../datasets") -> Dataset:
     """dbpedia-100k (1536-d) from a local file: $VQ_DATA_DIR/dbpedia-100k.{npy,fvecs}."""
-    root = Path(os.environ.get("VQ_DATA_DIR", cache_dir))
-    for name in ("dbpedia-100k.npy", "dbpedia-100k.fvecs", "dbpedia_100k.npy", "dbpedia_100k.fvecs"):
-        if (root / name).exists():
-            return load_local_dataset(root / name, limit=limit)
-    raise FileNotFoundError(
-        f"dbpedia-100k is fetched from the Hugging Face Hub by the reference; offline, place "
-        f"dbpedia-100k.npy or .fvecs under {root} (or set VQ_DATA_DIR)"
-    )
+    return load_named_dataset("dbpedia-100k", limit=limit, cache_dir=cache_dir)

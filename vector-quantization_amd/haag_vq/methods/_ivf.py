@@ -190,7 +190,9 @@ class IvfPq:
     # --------------------------------------------------------------- search
     def search(self, Q: torch.Tensor, k: int, nprobe: int) -> Tuple[torch.Tensor, torch.Tensor]:
         """(dists f32 (nq, k), ids int32 (nq, k)); L2 ascending, IP as negated scores."""
-        nprobe = max(1, min(int(nprobe), self.K, 256))
+        nprobe = max(1, min(int(nprobe), self.K))
+        if nprobe > 256:
+            raise ValueError(f"nprobe={nprobe}: the probe selection (mivq_topk_rows) supports at most 256 lists")
         pd, pl = _native.topk_rows(_native.pairwise_distances(Q, self.coarse, self.metric), nprobe)
         lut = _native.adc_lut(Q, self.pq, self.nbits, _native.METRIC_INNER_PRODUCT)
         L = self.lists

@@ -11,8 +11,10 @@ Drop-in for the reference's ``OptimizedProductQuantizer``
   then train a fresh PQ on the rotated data (:26-28).
 * compress = PQ encode of x . A^T (:31); decompress = PQ decode . A (:34).
 
-Hot path on device: the rotation is ``mivq_opq_rotate`` (fp32 GEMM, rocBLAS sgemm), encode /
-decode are the PQ kernels.  The Procrustes step of training (a D x D product and SVD) uses
+Hot path on device: the rotation is ``mivq_opq_rotate_prepared`` (hand-written split-f16
+MFMA GEMM with fp32 accuracy; the f16 hi / lo image of A is prepared once per matrix and
+direction), encode / decode are the PQ kernels.  ``mivq_opq_rotate`` (plain fp32 MFMA, no
+preparation) serves dimensions that are not multiples of 8.  The Procrustes step of training (a D x D product and SVD) uses
 the vendor libraries through torch — it is training, not the encode path.
 """
 
@@ -27,6 +29,17 @@ from .base_quantizer import BaseQuantizer
 from .product_quantization import ProductQuantizer
 
 
+def rotate(x: torch.Tensor, A: torch.Tensor, transpose: bool = False, prep=None,
+           out: torch.Tensor | None = None) -> torch.Tensor:
+    """x . A^T (transpose False) or x . A on the device: the prepared split-f16 GEMM when
+    A's image is available (d % 8 == 0), else the plain fp32 MFMA kernel."""
+    if prep is None:
+        prep = _native.opq_prepare(A, transpose)
+    if prep is None:
+        return _native.opq_rotate(x, A, transpose, out=out)
+    return _native.opq_rotate_prepared(x, prep, out=out)
+
+
 class OPQHandle:
     """Stands where the reference keeps ``faiss.OPQMatrix`` (``model.opq``)."""
 
@@ -34,6 +47,16 @@ class OPQHandle:
         self.A_device = A
         self.d_in = self.d_out = int(A.shape[0])
         self.is_orthonormal = True
+        self._prep = {}
+
+    def prep(self, transpose: bool):
+        """The prepared image of A^T (apply) or A (reverse), built on first use."""
+        if transpose not in self._prep:
+            self._prep[transpose] = _native.opq_prepare(self.A_device, transpose)
+        return self._prep[transpose]
+
+    def rotate(self, x: torch.Tensor, transpose: bool, out: torch.Tensor | None = None) -> torch.Tensor:
+        return rotate(x, self.A_device, transpose, prep=self.prep(transpose), out=out)
 
     @property
     def A(self) -> np.ndarray:
@@ -41,11 +64,11 @@ class OPQHandle:
 
     def _run(self, x, transpose: bool):
         if _arrays.is_tensor(x):
-            return _native.opq_rotate(_arrays.to_device(x), self.A_device, transpose)
+            return self.rotate(_arrays.to_device(x), transpose)
         x = np.asarray(x, dtype=np.float32)
         out = np.empty_like(x)
         for s, e in _arrays.row_chunks(x.shape[0], x.shape[1] * 8):
-            out[s:e] = _arrays.to_host(_native.opq_rotate(_arrays.to_device(x[s:e]), self.A_device, transpose))
+            out[s:e] = _arrays.to_host(self.rotate(_arrays.to_device(x[s:e]), transpose))
         return out
 
     def apply(self, x):
@@ -78,20 +101,29 @@ class OptimizedProductQuantizer(BaseQuantizer):
         if n > self.max_train_points:
             sel = np.sort(rng.permutation(n)[: self.max_train_points])
             X = X[torch.from_numpy(sel).to(X.device)].contiguous()
-        Q, _ = np.linalg.qr(np.random.default_rng(self.seed).standard_normal((d, d)))
-        A = torch.from_numpy(Q.astype(np.float32)).to(X.device).contiguous()
+        A = self.initial_rotation(d, X.device)
         C = None
         for it in range(self.niter):
-            Y = _native.opq_rotate(X, A, False)
-            C = train_pq(Y, self.M, self.B, niter=self.niter_pq_0 if it == 0 else self.niter_pq,
-                         seed=self.seed, max_points_per_centroid=1000, init=C)
-            prep = _native.pq_prepare(C, self.B)
-            Yhat = _native.pq_decode(_native.pq_encode(Y, C, prep, self.B), C, self.B)
-            # orthogonal Procrustes: argmin_R ||X R^T - Yhat||  ->  R = V U^T, X^T Yhat = U S V^T
-            G = (X.double().T @ Yhat.double())
-            U, _, Vh = torch.linalg.svd(G)
-            A = (Vh.T @ U.T).float().contiguous()
+            A, C, _, _ = self.train_step(X, A, C, it)
         return A
+
+    def initial_rotation(self, d: int, device) -> torch.Tensor:
+        """Random orthonormal start (QR of a seeded Gaussian matrix)."""
+        Q, _ = np.linalg.qr(np.random.default_rng(self.seed).standard_normal((d, d)))
+        return torch.from_numpy(Q.astype(np.float32)).to(device).contiguous()
+
+    def train_step(self, X: torch.Tensor, A: torch.Tensor, C, it: int):
+        """One round of the alternating optimisation: rotate, (re)train PQ on the rotated
+        sample, encode + decode, orthogonal-Procrustes update.  Returns (A', C, Y, Yhat)."""
+        Y = rotate(X, A, False)
+        C = train_pq(Y, self.M, self.B, niter=self.niter_pq_0 if it == 0 else self.niter_pq,
+                     seed=self.seed, max_points_per_centroid=1000, init=C)
+        prep = _native.pq_prepare(C, self.B)
+        Yhat = _native.pq_decode(_native.pq_encode(Y, C, prep, self.B), C, self.B)
+        # orthogonal Procrustes: argmin_R ||X R^T - Yhat||  ->  R = V U^T, X^T Yhat = U S V^T
+        G = (X.double().T @ Yhat.double())
+        U, _, Vh = torch.linalg.svd(G)
+        return (Vh.T @ U.T).float().contiguous(), C, Y, Yhat
 
     def fit(self, X) -> None:
         Xd = _arrays.to_device(X, torch.float32)
@@ -100,7 +132,7 @@ class OptimizedProductQuantizer(BaseQuantizer):
         A = self._train_rotation(Xd)
         self.opq = OPQHandle(A)
         inner = ProductQuantizer(M=self.M, B=self.B)
-        inner.fit(_native.opq_rotate(Xd, A, False))
+        inner.fit(self.opq.rotate(Xd, False))
         self._inner = inner
         self.pq = inner.pq
 
@@ -115,7 +147,7 @@ class OptimizedProductQuantizer(BaseQuantizer):
         X = np.asarray(X, dtype=np.float32)
         out = np.empty((X.shape[0], _native.pq_code_size(self.M, self.B)), dtype=np.uint8)
         for s, e in _arrays.row_chunks(X.shape[0], X.shape[1] * 8):
-            y = _native.opq_rotate(_arrays.to_device(X[s:e]), self.opq.A_device, False)
+            y = self.opq.rotate(_arrays.to_device(X[s:e]), False)
             out[s:e] = _arrays.to_host(self._inner.compress(y))
         return out
 

@@ -47,6 +47,8 @@ def search_codes(model: BaseQuantizer, codes, Q, k: int, metric: str = "l2") -> 
     Qd = _arrays.to_device(Q)
     cd = codes if _arrays.is_tensor(codes) else torch.from_numpy(np.ascontiguousarray(codes))
     cd = cd.to(_arrays.device())
+    if k > MAX_KERNEL_K:
+        return _search_large_k(model, cd, Qd, k, mt)
     if isinstance(model, (ProductQuantizer, OptimizedProductQuantizer)):
         pq = model if isinstance(model, ProductQuantizer) else model.inner
         if isinstance(model, OptimizedProductQuantizer):
@@ -59,6 +61,29 @@ def search_codes(model: BaseQuantizer, codes, Q, k: int, metric: str = "l2") -> 
         xh = model.decompress(cd)
         xh = _arrays.to_device(xh, torch.float32)
         d, i = _native.flat_search(Qd, xh, k, mt)
+    if mt == _native.METRIC_INNER_PRODUCT:
+        d = -d
+    return d, i
+
+
+MAX_KERNEL_K = 256  # the wave-resident top-k of the scan kernels
+
+
+def _search_large_k(model, cd, Qd, k: int, mt: int) -> Tuple[torch.Tensor, torch.Tensor]:
+    """k > 256 (the reference's cdist + argpartition has no limit): decode once, exact
+    (query, row) distances with mivq_pairwise_distances in query blocks, and a stable
+    device sort, so ties keep the smaller id first."""
+    xh = _arrays.to_device(model.decompress(cd), torch.float32)
+    n = xh.shape[0]
+    k = min(k, n)
+    block = max(1, (1 << 28) // max(1, n))
+    ds, is_ = [], []
+    for s in range(0, Qd.shape[0], block):
+        D = _native.pairwise_distances(Qd[s:s + block].contiguous(), xh, mt)
+        v, i = torch.sort(D, dim=1, stable=True)
+        ds.append(v[:, :k].contiguous())
+        is_.append(i[:, :k].to(torch.int32).contiguous())
+    d, i = torch.cat(ds), torch.cat(is_)
     if mt == _native.METRIC_INNER_PRODUCT:
         d = -d
     return d, i

@@ -10,8 +10,10 @@ rescale factor t, MSB-first packing) and the mirror image for decode.  Code rows
 ``ceil(D*B/8) + 8`` bytes (indices ++ f32 norm ++ f32 t) and decode row-independently.
 
 Parity: fp64 throughout; the GEMM's summation order differs from numpy/OpenBLAS, so an index
-can differ only where s lies within rounding distance of a level midpoint ("tie-aware", counted
-in tests/test_quantizers_gpu.py), and the decoded vectors agree to ~1e-12 relative.
+can differ only where s lies within rounding distance of a level midpoint (each such index is
+checked to be a midpoint tie against the reference's fixtures in
+tests/test_pinning_gpu.py::test_extrabitq_mismatches_are_midpoint_ties), and the decoded
+vectors agree to ~1e-12 relative.
 """
 
 from __future__ import annotations

@@ -15,7 +15,11 @@ extern "C" __attribute__((visibility("default"))) int cs_variant(int V, const fl
                                                                   uint8_t* codesT, void* items, void* counts, void* pinfo,
                                                                   void* st) {
     switch (V) {
-        VARIANT(0) VARIANT(1) VARIANT(2) VARIANT(4) VARIANT(8) VARIANT(17) VARIANT(33) VARIANT(65) VARIANT(145) VARIANT(256) VARIANT(513) VARIANT(1537) VARIANT(2561) VARIANT(4609) VARIANT(7681) VARIANT(16384) VARIANT(32768) VARIANT(65536) VARIANT(131073) VARIANT(131072) VARIANT(262144)
+#ifdef CS_VARIANTS
+        CS_VARIANTS
+#else
+        VARIANT(0) VARIANT(1) VARIANT(2) VARIANT(4) VARIANT(8) VARIANT(17) VARIANT(33) VARIANT(65) VARIANT(145) VARIANT(256) VARIANT(513) VARIANT(1537) VARIANT(2561) VARIANT(4609) VARIANT(7681) VARIANT(16384) VARIANT(32768) VARIANT(65536) VARIANT(131073) VARIANT(131072) VARIANT(262144) VARIANT(1048576) VARIANT(2097152) VARIANT(4194304) VARIANT(8388608) VARIANT(6291456)
+#endif
         default: return -1;
     }
 }

@@ -25,7 +25,8 @@ VARIANTS = {0: "encode + resolve", 1: "encode only", 2: "resolve: pairs only", 4
             145: "streaming only, subspace-major probe", 256: "encode + resolve, 256-wide full scans",
             513: "encode + full-item kernel", 1537: "... no exact chains", 2561: "... 1 of 8 filter blocks",
             4609: "... no gathers", 7681: "... none of the three", 16384: "encode + resolve, lane-wide top-3 filter", 32768: "encode + resolve, no pair window", 65536: "encode + resolve, LDS-codebook full-item kernel",
-            131073: "encode only, A fragments of block 0 reused (LDS probe)", 131072: "encode + resolve, A fragments reused"}
+            131073: "encode only, A fragments of block 0 reused (LDS probe)", 131072: "encode + resolve, A fragments reused",
+            1048576: "round-1 resolve (pair window in the pair kernel, full2 + pair kernels)"}
 
 
 def prep_layout(M, dsub, ksub=256):
@@ -45,6 +46,8 @@ def prep_layout(M, dsub, ksub=256):
 
 
 def build(lib=None):
+    """tools/build/libcsvar.so (all variants), or --lib: a prebuilt one, e.g. built with only the
+    variants at hand:  hipcc ... -DCS_VARIANTS="VARIANT(0) VARIANT(1)" -o tools/build/x.so"""
     if lib:
         return ctypes.CDLL(str(ROOT / lib))
     so = ROOT / "tools" / "build" / "libcsvar.so"

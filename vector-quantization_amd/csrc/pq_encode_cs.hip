@@ -9,7 +9,7 @@
 // (blockIdx = chunk*M + m).  The number of chunks is chosen so that the grid is a whole
 // number of rounds of workgroups over the CUs (one workgroup per CU: the LDS below).
 //
-// Phase 1 (streaming).  LDS holds, for the workgroup's life,
+// Launch 1, the filter (streaming).  LDS holds, for the workgroup's life,
 //   cimg : the fp16 operand image of C_m in fragment order (8*KS KiB; ds_read_b128)
 //   stg  : one fp16 x tile per wave, 32 rows x 16*KS halves, row pitch 32*KS+16 bytes
 //   hb   : the scaled accumulator init -|c|^2 * sigma * tau / 2;  cnl : |c|^2
@@ -20,19 +20,21 @@
 // and written to the wave's tile (tile rows past the range keep stale values: an MFMA
 // column depends on its own row only); the MFMA B fragments are read back from it.  The next
 // vb's loads are in flight while the current one is filtered: 8*KS v_mfma_f32_32x32x16_f16,
-// a packed top-3 per lane (one v_and_or_b32 + max + 2 med3 per score), the partner-lane
-// merge, then
+// a grouped top-2 / lane top-3 per lane, the partner-lane merge, then
 //   1 candidate in the window -> the code is written;
-//   2 candidates              -> (row, k1, k2) goes to the workgroup's pair list;
+//   2 candidates              -> the pair is held for one step while the 8-B load of its
+//                                pair spreads is in flight; if the score gap exceeds the
+//                                pair's own window, k1 is the code, else (row, k1, k2) goes
+//                                to the workgroup's pair list;
 //   >= 3 candidates, or a row the window cannot bound (fp16 overflow, NaN) -> full list.
-// Phase 2 (resolve).  The LDS is re-staged with the exact fp32 codebook, centroid pairs
-// (k, k+128) interleaved, and the workgroup settles its lists, one item per lane, with the
-// canonical fmaf chains: pairs compare their two candidates, full items scan all 256
-// centroids with v_pk_fma_f32 (two chains per instruction, LDS broadcast reads).  The x
-// sub-row is re-read from memory (about 11% of the rows on embedding-like data).
-// Codes go to a transposed (M, n) scratch (32 contiguous bytes per vb); a transpose kernel
-// writes the (n, M) layout.  Lists live in a workspace of n*M uint2 (workgroup (c, m) owns
-// entries m*n + [r0, r1): pairs from the front, full items from the back).
+// Launch 2, pq_resolve_merged_kernel: one workgroup per filter workgroup settles both lists
+// with the canonical fp32 chains (fp32 codebook in LDS), re-running the filter for full
+// items to list the centroids inside the window.  Launch 3 transposes the codes.
+// Codes go to a transposed (M, n) scratch (32 contiguous bytes per vb); lists live in a
+// workspace of n*M uint2 (workgroup (c, m) owns entries m*n + [r0, r1): pairs from the
+// front, full items from the back).
+// (Measured and dropped: a consumer wave inside the filter workgroup settling the items while
+// the other 11 waves stream -- the filter lost 13 % and the consumer could not keep up.)
 #include "pq_internal.h"
 
 #include <math.h>
@@ -176,6 +178,8 @@ constexpr int max_loads() {
     return (32 + (16 / KS) - 1) / (16 / KS);
 }
 
+constexpr int kLCap = 8;  // candidates per lane (128 centroids); more -> the lane scans all of them
+
 // V: profiling variants (tools/cs_variants.hip), 0 in the library.  Bits drop work and
 // produce wrong codes: 1 the resolve kernel, 2 its full scans, 4 its pair checks, 8 its x
 // reads, 16 the whole filter, 32 all but the first 32 centroids of the filter, 64 the x
@@ -197,7 +201,8 @@ __global__ __launch_bounds__(kThreads) void pq_encode_cs_kernel(
     const float* __restrict__ x, int64_t n, int d, int M, int dsub_in, int64_t rows_per_wg,
     const float* __restrict__ C, const float* __restrict__ cn, const half8* __restrict__ img,
     const float* __restrict__ hinit, const float4* __restrict__ bnd, uint8_t* __restrict__ codesT,
-    uint2* __restrict__ items, int2* __restrict__ counts, float2* __restrict__ pinfo) {
+    uint2* __restrict__ items, int2* __restrict__ counts, float2* __restrict__ pinfo,
+    const float2* __restrict__ pdw, const float4* __restrict__ bnd2) {
     constexpr int FR = 8 * KS * 64;
     constexpr int PITCH = 32 * KS + 16;  // bytes per fp16 tile row (16 B pad: conflict-free reads)
     constexpr int NIMAX = LAYOUT == 0 ? max_loads<KS>() : 2 * KS;
@@ -207,6 +212,7 @@ __global__ __launch_bounds__(kThreads) void pq_encode_cs_kernel(
     float* hb = reinterpret_cast<float*>(stg_all + kWaves * 32 * PITCH);
     float* cnl = hb + 256;
     int* ctr = reinterpret_cast<int*>(cnl + 256);  // [0] pairs, [1] full, [2] resolve batches
+    constexpr int kProd = kWaves;  // streaming waves
 
     const int dsub = DS > 0 ? DS : dsub_in;
     const int tid = threadIdx.x;
@@ -232,6 +238,7 @@ __global__ __launch_bounds__(kThreads) void pq_encode_cs_kernel(
         if (tid < 4) ctr[tid] = 0;
     }
     __syncthreads();
+    {
 
     // ------------------------------------------------------------------ phase 1: stream
     // Load geometry.  LAYOUT 0: instruction i reads rows rpi*i + [0, rpi), lanes past
@@ -290,6 +297,50 @@ __global__ __launch_bounds__(kThreads) void pq_encode_cs_kernel(
         }
     };
 
+    // Pair window inside the filter (pdw != null): a row with exactly two candidates is held
+    // for one step while the 8-B load of its pair spreads {||c~_k1 - c~_k2||, ||dc_k1 - dc_k2||}
+    // (pq_prep_spread_kernel) is in flight; if the score gap exceeds the pair's own f16
+    // rounding bound, k1 is the code and the row never reaches the resolve kernel.
+    int pend_row = -1, pend_k = 0;
+    float pend_gap = 0.0f, pend_xs = 0.0f;
+    float2 pend_pd = make_float2(0.0f, 0.0f);
+    const float4 b2 = pdw != nullptr ? bnd2[m] : make_float4(0.f, 0.f, 0.f, 0.f);
+    auto settle_pending = [&]() __attribute__((always_inline)) {
+        if (pend_row < 0) return false;
+        const float w12 = 1.0625f * (fmaf(4.8828125e-4f, pend_xs, b2.z) * pend_pd.x + pend_xs * pend_pd.y +
+                                     b2.x * pend_xs + b2.y);
+        if (pend_gap > w12) {
+            codesT[(int64_t)m * n + r0 + pend_row] = (uint8_t)(pend_k & 0xFF);
+            return false;
+        }
+        return true;
+    };
+    // Appends this wave's pair items (row prow, candidates pk) and full items (row frow) to the
+    // workgroup's lists: pairs from the front, full items from the back.
+    auto append = [&](bool isp, int prow, int pk, float pgap, float pxs, bool isf, int frow)
+                      __attribute__((always_inline)) {
+        const uint64_t bp = __ballot(isp);
+        const uint64_t bfull = __ballot(isf);
+        if (bp | bfull) {
+            int basep = 0, basef = 0;
+            if (l == 0) {
+                if (bp) basep = atomicAdd(&ctr[0], __popcll(bp));
+                if (bfull) basef = atomicAdd(&ctr[1], __popcll(bfull));
+            }
+            basep = __shfl(basep, 0);
+            basef = __shfl(basef, 0);
+            const uint64_t below = (1ull << l) - 1ull;
+            uint2* list = items + (int64_t)m * n + r0;
+            if (isp) {
+                const int at = basep + __popcll(bp & below);
+                list[at] = make_uint2((uint32_t)prow, (uint32_t)pk);
+                // the legacy pair kernel's own window needs the score gap and Xs
+                if (pdw == nullptr) pinfo[(int64_t)m * n + r0 + at] = make_float2(pgap, pxs);
+            }
+            if (isf) list[nrows - 1 - (basef + __popcll(bfull & below))] = make_uint2((uint32_t)frow, 0u);
+        }
+    };
+
     // One step encodes block vb from registers xr and refills xr with block vb + kDepth*kWaves
     // right after staging it, so kDepth blocks per wave are in flight.
     auto step = [&](const int vb, float4 (&xr)[NIMAX]) __attribute__((always_inline)) {
@@ -323,7 +374,7 @@ __global__ __launch_bounds__(kThreads) void pq_encode_cs_kernel(
             xx = dot2_self(u[0], xx); xx = dot2_self(u[1], xx);
             xx = dot2_self(u[2], xx); xx = dot2_self(u[3], xx);
         }
-        if (vb + kDepth * kWaves < nvb && !((V & 64) && vb >= kWaves)) load(vb + kDepth * kWaves, xr);
+        if (vb + kDepth * kProd < nvb && !((V & 64) && vb >= kProd)) load(vb + kDepth * kProd, xr);
         xx += __shfl_xor(xx, 32);
 
         // Candidates: the 16 packed scores of centroid block cb in this lane form a group; each
@@ -411,37 +462,40 @@ __global__ __launch_bounds__(kThreads) void pq_encode_cs_kernel(
         const int rowl = vb * 32 + r;
         const bool mine = (h == 0) && rowl < nrows;
         if (mine && ncand == 1) codesT[(int64_t)m * n + r0 + rowl] = (uint8_t)k1;
-        const uint64_t bp = __ballot(mine && ncand == 2);
-        const uint64_t bfull = __ballot(mine && ncand >= 3);
-        if (bp | bfull) {
-            int basep = 0, basef = 0;
-            if (l == 0) {
-                if (bp) basep = atomicAdd(&ctr[0], __popcll(bp));
-                if (bfull) basef = atomicAdd(&ctr[1], __popcll(bfull));
+        const float gap = __fmul_rn(__fsub_rn(t1, t2), 0.99999988f);  // rounded down
+        if (pdw != nullptr) {
+            // The previous block's pair (its pd load was issued a whole step ago): k1 is the
+            // code when the gap exceeds the pair's own window, else it goes to the list.
+            const bool listp = settle_pending();
+            append(listp, pend_row, pend_k, 0.0f, 0.0f, mine && ncand >= 3, rowl);
+            pend_row = (mine && ncand == 2) ? rowl : -1;
+            if (pend_row >= 0) {
+                pend_k = k1 | (k2 << 8);
+                pend_gap = gap;
+                pend_xs = Xs;
+                pend_pd = pdw[((int64_t)m * 256 + k1) * 256 + k2];
             }
-            basep = __shfl(basep, 0);
-            basef = __shfl(basef, 0);
-            const uint64_t below = (1ull << l) - 1ull;
-            uint2* list = items + (int64_t)m * n + r0;
-            if (mine && ncand == 2) {
-                // the pair kernel's own window needs the score gap (rounded down) and Xs
-                const int at = basep + __popcll(bp & below);
-                list[at] = make_uint2((uint32_t)rowl, (uint32_t)(k1 | (k2 << 8)));
-                pinfo[(int64_t)m * n + r0 + at] = make_float2(__fmul_rn(__fsub_rn(t1, t2), 0.99999988f), Xs);  // gap rounded down
-            }
-            if (mine && ncand >= 3) list[nrows - 1 - (basef + __popcll(bfull & below))] = make_uint2((uint32_t)rowl, 0u);
+        } else {
+            append(mine && ncand == 2, rowl, k1 | (k2 << 8), gap, Xs, mine && ncand >= 3, rowl);
         }
     };
-    float4 xa[NIMAX], xb[NIMAX];
-    int vb = w;
-    if (vb < nvb) load(vb, xa);
-    if (kDepth == 2 && vb + kWaves < nvb) load(vb + kWaves, xb);
-    for (; vb < nvb; vb += kDepth * kWaves) {
-        step(vb, xa);
-        if (kDepth == 1) continue;
-        if (vb + kWaves >= nvb) break;
-        step(vb + kWaves, xb);
+    {
+        float4 xa[NIMAX], xb[NIMAX];
+        int vb = w;
+        if (vb < nvb) load(vb, xa);
+        if (kDepth == 2 && vb + kProd < nvb) load(vb + kProd, xb);
+        for (; vb < nvb; vb += kDepth * kProd) {
+            step(vb, xa);
+            if (kDepth == 1) continue;
+            if (vb + kProd >= nvb) break;
+            step(vb + kProd, xb);
+        }
+        if (pdw != nullptr) {
+            const bool listp = settle_pending();
+            append(listp, pend_row, pend_k, 0.0f, 0.0f, false, 0);
+        }
     }
+    }  // producers
     __syncthreads();
     if (tid == 0) counts[blockIdx.x] = make_int2(ctr[0], ctr[1]);
 }
@@ -1139,6 +1193,312 @@ __global__ __launch_bounds__(kFWaves * 64) __attribute__((amdgpu_waves_per_eu(2)
     }
 }
 
+// Merged resolve (the library default): one launch settles a workgroup's full items and the
+// pairs its filter could not settle with the pair window.  One workgroup (4 waves, one per
+// SIMD: up to 512 registers per lane) per encode workgroup; LDS holds the exact fp32 codebook
+// C_m (the canonical chains of both kinds read it), the norms, the accumulator init, and per
+// wave a 32-row fp32 staging tile plus a candidate list.  A full batch loads the filter's f16 A
+// operands of all 8 centroid blocks (192 registers at KS = 6, from the L2-resident prepared
+// image) together with its row gather.
+//   full batch (32 rows): gather the rows, build the B operand exactly as the filter does, one
+//     MFMA sweep with all 8 accumulators kept, t1 = max, every centroid inside the window
+//     (score >= t1 - W) goes to the row's candidate list; the two lanes of a row then run the
+//     canonical chains of alternate candidates and merge (s, k).  Every minimiser of the
+//     canonical score lies inside the window, so the smallest (s, k) is the canonical code.
+//     Rows the window cannot vouch for (non-finite, out of range) or with more than kFCap
+//     candidates are scanned over all 256 centroids.
+//   pair batch (32 rows): lane (r, 0) runs the chain of k1, lane (r, 1) that of k2; merge.
+constexpr int kMWaves = 4;
+
+template <int KS>
+constexpr int merged_smem_bytes() {
+    return 256 * (16 * KS) * 4 + 2 * 256 * 4 + 16 + kMWaves * (32 * (16 * KS + 4) * 4 + 64 * (kLCap + 1) * 4);
+}
+
+// V (profiling, tools/cs_variants.hip): 1 << 21 skips the full batches, 1 << 22 the pair
+// batches, 1 << 23 does the gathers only (no MFMA, no chains), 1 << 24 skips the full
+// batches' chains, 1 << 25 their candidate collection and chains (wrong codes).
+template <int KS, int DS, int V = 0>
+__global__ __launch_bounds__(kMWaves * 64) __attribute__((amdgpu_waves_per_eu(1, 1))) void pq_resolve_merged_kernel(
+    const float* __restrict__ x, int64_t n, int d, int M, int dsub_in, int64_t rows_per_wg,
+    const float* __restrict__ C, const float* __restrict__ cn, const half8* __restrict__ img,
+    const float* __restrict__ hinit, const float4* __restrict__ bnd, uint8_t* __restrict__ codesT,
+    const uint2* __restrict__ items, const int2* __restrict__ counts) {
+    constexpr int DP = 16 * KS;  // padded dsub
+    constexpr int XP = DP + 4;   // floats per staged x row
+    constexpr int NL = 2 * KS;   // 16-B loads per lane per 32-row gather
+    constexpr int FR = 8 * KS * 64;
+    const int dsub = DS > 0 ? DS : dsub_in;
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    float* cl = reinterpret_cast<float*>(smem);  // [256][DP]
+    float* cnl = cl + 256 * DP;
+    float* hb = cnl + 256;
+    int* ctr = reinterpret_cast<int*>(hb + 256);
+    const int tid = threadIdx.x;
+    const int w = __builtin_amdgcn_readfirstlane(tid >> 6), l = tid & 63;
+    const int r = l & 31, h = l >> 5;
+    float* xf = reinterpret_cast<float*>(reinterpret_cast<unsigned char*>(ctr + 4) +
+                                         w * (32 * XP * 4 + 64 * (kLCap + 1) * 4));
+    int* cand = reinterpret_cast<int*>(xf + 32 * XP) + l * (kLCap + 1);  // this lane's list + a sink slot
+
+    int m;
+    int64_t chunk;
+    wg_coords(M, m, chunk);
+    const int64_t r0 = chunk * rows_per_wg;
+    const int64_t r1 = min(n, r0 + rows_per_wg);
+    if (r0 >= r1) return;
+    const int nrows = (int)(r1 - r0);
+    const int2 cnt = counts[blockIdx.x];
+    const int np = cnt.x, nf = cnt.y;
+    if (np + nf == 0) return;
+    const float* Cm = C + (int64_t)m * 256 * dsub;
+    {  // the fp32 codebook, zero-padded to DP; 16-B copies, 8 in flight per thread
+        const int q4 = DP >> 2, tot = 256 * q4;
+        for (int e0 = tid; e0 < tot; e0 += 8 * kMWaves * 64) {
+            f32x4 v[8];
+#pragma unroll
+            for (int u = 0; u < 8; ++u) {
+                const int e = e0 + u * kMWaves * 64;
+                const int k = e / q4, j = e - k * q4;
+                v[u] = (e < tot && 4 * j < dsub) ? *reinterpret_cast<const f32x4*>(Cm + (int64_t)k * dsub + 4 * j)
+                                                 : (f32x4){0.f, 0.f, 0.f, 0.f};
+            }
+#pragma unroll
+            for (int u = 0; u < 8; ++u) {
+                const int e = e0 + u * kMWaves * 64;
+                if (e < tot) *reinterpret_cast<f32x4*>(cl + 4 * e) = v[u];
+            }
+        }
+        cnl[tid] = cn[(int64_t)m * 256 + tid];
+        hb[tid] = hinit[(int64_t)m * 256 + tid];
+        if (tid == 0) ctr[0] = 0;
+    }
+    __syncthreads();
+    const half8* im = img + (int64_t)m * FR;
+
+    const float4 bm = bnd[m];
+    const float2v sig2 = {bm.x, bm.x};
+    const float xs_eta = 5.9604645e-8f * sqrtf((float)dsub);
+    const int q = dsub >> 2;
+    const int nld = (32 * q + 63) >> 6;
+    const uint2* list = items + (int64_t)m * n + r0;
+    const float* xsub = x + r0 * d + (int64_t)m * dsub;
+    const int nbf = (nf + 31) >> 5, nbp = (np + 31) >> 5;
+
+    // canonical score of centroid k for the row xv held in registers (DS > 0: the whole
+    // centroid row is read first, then the sequential fmaf chain runs without waits)
+    constexpr int NQ = DS > 0 ? DS / 4 : 1;
+    auto exact_reg = [&](const f32x4 (&xv)[NQ], int k) __attribute__((always_inline)) {
+        const float* c = cl + k * DP;
+        f32x4 cv[NQ];
+#pragma unroll
+        for (int t = 0; t < NQ; ++t) cv[t] = *reinterpret_cast<const f32x4*>(c + 4 * t);
+        float dot = 0.0f;
+#pragma unroll
+        for (int t = 0; t < NQ; ++t) {
+            dot = __builtin_fmaf(xv[t].x, cv[t].x, dot);
+            dot = __builtin_fmaf(xv[t].y, cv[t].y, dot);
+            dot = __builtin_fmaf(xv[t].z, cv[t].z, dot);
+            dot = __builtin_fmaf(xv[t].w, cv[t].w, dot);
+        }
+        return __builtin_fmaf(-2.0f, dot, cnl[k]);
+    };
+    auto load_row = [&](const float* xr, f32x4 (&xv)[NQ]) __attribute__((always_inline)) {
+#pragma unroll
+        for (int t = 0; t < NQ; ++t) xv[t] = *reinterpret_cast<const f32x4*>(xr + 4 * t);
+    };
+    // canonical score of centroid k for the staged row xr (sequential fmaf chain over t), any dsub
+    auto exact = [&](const float* xr, int k) __attribute__((always_inline)) {
+        const float* c = cl + k * DP;
+        float dot = 0.0f;
+#pragma unroll 2
+        for (int t = 0; t < (DS > 0 ? DS : dsub); t += 4) {
+            const f32x4 cv = *reinterpret_cast<const f32x4*>(c + t);
+            const f32x4 xv = *reinterpret_cast<const f32x4*>(xr + t);
+            dot = __builtin_fmaf(xv.x, cv.x, dot);
+            dot = __builtin_fmaf(xv.y, cv.y, dot);
+            dot = __builtin_fmaf(xv.z, cv.z, dot);
+            dot = __builtin_fmaf(xv.w, cv.w, dot);
+        }
+        return __builtin_fmaf(-2.0f, dot, cnl[k]);
+    };
+    // 32 sub-rows (row offsets in rowl of lanes 0..cntb-1) into the wave's staging tile
+    auto gather = [&](int cntb, int rowl) __attribute__((always_inline)) {
+        f32x4 v[NL];
+#pragma unroll
+        for (int j = 0; j < NL; ++j) {
+            const int c = j * 64 + l;
+            const int row = c / q, col = c - row * q;
+            const int src = __shfl(rowl, min(row, 31));
+            const bool ok = j < nld && row < cntb;
+            v[j] = *reinterpret_cast<const f32x4*>(xsub + (ok ? (int64_t)src * d + 4 * col : 0));
+        }
+#pragma unroll
+        for (int j = 0; j < NL; ++j) {
+            const int c = j * 64 + l;
+            const int row = c / q, col = c - row * q;
+            if (j < nld && row < 32) *reinterpret_cast<f32x4*>(xf + row * XP + 4 * col) = v[j];
+        }
+        if (DS == 0 || DS != DP)
+            for (int e = l; e < 32 * (DP - dsub); e += 64) {
+                const int row = e / (DP - dsub);
+                xf[row * XP + dsub + (e - row * (DP - dsub))] = 0.0f;
+            }
+        lds_fence();
+    };
+
+    for (;;) {
+        int b = 0;
+        if (l == 0) b = atomicAdd(&ctr[0], 1);
+        b = __shfl(b, 0);
+        if (b >= nbf + nbp) break;
+        const float* xr = xf + r * XP;
+        if constexpr ((V & (3 << 21)) != 0) {
+            if (((V & (1 << 21)) && b < nbf) || ((V & (1 << 22)) && b >= nbf)) continue;
+        }
+        if constexpr ((V & (1 << 23)) != 0) {
+            const int first = (b < nbf ? b : b - nbf) * 32;
+            const int cntb = min(32, (b < nbf ? nf : np) - first);
+            int rowl = 0;
+            if (l < cntb) rowl = (int)(b < nbf ? list[nrows - 1 - (first + l)].x : list[first + l].x);
+            gather(cntb, rowl);
+            continue;
+        }
+        if (b < nbf) {
+            const int first = b * 32;
+            const int cntb = min(32, nf - first);
+            int rowl = 0;
+            if (l < cntb) rowl = (int)list[nrows - 1 - (first + l)].x;
+            gather(cntb, rowl);
+            // the filter's A operands (the prepared f16 image of C_m, L2-resident), all 8
+            // centroid blocks, in flight while the B operand is built
+            half8 aa[8][KS];
+#pragma unroll
+            for (int cb = 0; cb < 8; ++cb)
+#pragma unroll
+                for (int ks = 0; ks < KS; ++ks) aa[cb][ks] = im[(cb * KS + ks) * 64 + l];
+            half8 bf[KS];
+            float xx = 0.0f;
+#pragma unroll
+            for (int ks = 0; ks < KS; ++ks) {
+                const float* src = xr + h * 8 * KS + 8 * ks;
+                const f32x4 a0 = *reinterpret_cast<const f32x4*>(src);
+                const f32x4 a1 = *reinterpret_cast<const f32x4*>(src + 4);
+                const float2v p0 = (float2v){a0.x, a0.y} * sig2, p1 = (float2v){a0.z, a0.w} * sig2;
+                const float2v p2 = (float2v){a1.x, a1.y} * sig2, p3 = (float2v){a1.z, a1.w} * sig2;
+                const u32x4 u = (u32x4){cvt2(p0.x, p0.y), cvt2(p1.x, p1.y), cvt2(p2.x, p2.y), cvt2(p3.x, p3.y)};
+                bf[ks] = __builtin_bit_cast(half8, u);
+                xx = dot2_self(u[0], xx); xx = dot2_self(u[1], xx);
+                xx = dot2_self(u[2], xx); xx = dot2_self(u[3], xx);
+            }
+            xx += __shfl_xor(xx, 32);
+            floatx16 acc[8];
+#pragma unroll
+            for (int cb = 0; cb < 8; ++cb) {
+#pragma unroll
+                for (int qq = 0; qq < 4; ++qq) {
+                    const float4 hv = *reinterpret_cast<const float4*>(hb + cb * 32 + 8 * qq + 4 * h);
+                    acc[cb][4 * qq + 0] = hv.x; acc[cb][4 * qq + 1] = hv.y;
+                    acc[cb][4 * qq + 2] = hv.z; acc[cb][4 * qq + 3] = hv.w;
+                }
+            }
+#pragma unroll
+            for (int ks = 0; ks < KS; ++ks)
+#pragma unroll
+                for (int cb = 0; cb < 8; ++cb)
+                    acc[cb] = __builtin_amdgcn_mfma_f32_32x32x16_f16(aa[cb][ks], bf[ks], acc[cb], 0, 0, 0);
+            float t1 = -INFINITY;
+#pragma unroll
+            for (int cb = 0; cb < 8; ++cb)
+#pragma unroll
+                for (int i = 0; i < 16; ++i) t1 = fmaxf(t1, acc[cb][i]);
+            t1 = fmaxf(t1, __shfl_xor(t1, 32));
+            const float Xs = (sqrtf(xx) * (1.0f + 1e-5f) + xs_eta) * (1.0f + 9.765625e-4f);
+            const float W = bm.y * Xs + bm.z;
+            const float thr = t1 - W;
+            const bool bad = !(Xs < 65000.0f) || !isfinite(t1) || !isfinite(W);
+            if constexpr ((V & (1 << 25)) != 0) {
+                if (h == 0 && r < cntb) codesT[(int64_t)m * n + r0 + rowl] = (uint8_t)(__float_as_uint(thr) & 0xFF);
+                lds_fence();
+                continue;
+            }
+            // this lane's centroids inside the window, appended without branches (the slot
+            // after the list is a sink); the lane then runs their canonical chains
+            int nc = 0;
+#pragma unroll
+            for (int cb = 0; cb < 8; ++cb) {
+#pragma unroll
+                for (int i = 0; i < 16; ++i) {
+                    const bool in = acc[cb][i] >= thr;
+                    cand[in ? min(nc, kLCap - 1) : kLCap] = cb * 32 + (i & 3) + 8 * (i >> 2) + 4 * h;
+                    nc += in ? 1 : 0;
+                }
+            }
+            lds_fence();
+            float bs = INFINITY;
+            int bk = 256;
+            auto take = [&](float sc, int k) __attribute__((always_inline)) {
+                if (sc < bs || (sc == bs && k < bk)) { bs = sc; bk = k; }
+            };
+            if (r < cntb && !(V & (1 << 24))) {
+                if (bad || nc > kLCap) {
+                    // the lane's 128 centroids, increasing k
+                    for (int cb = 0; cb < 8; ++cb)
+                        for (int qq = 0; qq < 4; ++qq)
+                            for (int e = 0; e < 4; ++e) {
+                                const int k = cb * 32 + 8 * qq + 4 * h + e;
+                                take(exact(xr, k), k);
+                            }
+                } else if constexpr (DS > 0) {
+                    f32x4 xv[NQ];
+                    load_row(xr, xv);
+                    for (int j = 0; j < nc; ++j) {
+                        const int k = cand[j];
+                        take(exact_reg(xv, k), k);
+                    }
+                } else {
+                    for (int j = 0; j < nc; ++j) {
+                        const int k = cand[j];
+                        take(exact(xr, k), k);
+                    }
+                }
+            }
+            const float os = __shfl_xor(bs, 32);
+            const int ok = __shfl_xor(bk, 32);
+            if (os < bs || (os == bs && ok < bk)) { bs = os; bk = ok; }
+            if (h == 0 && r < cntb) codesT[(int64_t)m * n + r0 + rowl] = (uint8_t)((bs < INFINITY) ? bk : 0);
+            lds_fence();
+        } else {
+            // 32 pairs: lane (r, 0) runs the chain of k1, lane (r, 1) that of k2
+            const int first = (b - nbf) * 32;
+            const int cntb = min(32, np - first);
+            uint2 it = make_uint2(0u, 0u);
+            if (r < cntb) it = list[first + r];
+            const int rowl = (int)it.x;
+            gather(cntb, rowl);
+            const int k1 = (int)(it.y & 0xFFu), k2 = (int)((it.y >> 8) & 0xFFu);
+            const int kk = h ? k2 : k1;
+            float sc = 0.0f;
+            if (r < cntb) {
+                if constexpr (DS > 0) {
+                    f32x4 xv[NQ];
+                    load_row(xr, xv);
+                    sc = exact_reg(xv, kk);
+                } else {
+                    sc = exact(xr, kk);
+                }
+            }
+            const float os = __shfl_xor(sc, 32);
+            if (h == 0 && r < cntb) {
+                // (s1, k1) here, (s2, k2) from the partner: smallest (s, k), NaN never wins
+                const bool two = os < sc || (os == sc && k2 < k1) || (sc != sc && os == os);
+                codesT[(int64_t)m * n + r0 + rowl] = (uint8_t)(two ? k2 : k1);
+            }
+            lds_fence();
+        }
+    }
+}
+
 // (M, n) -> (n, M): one block per 256 rows, the tile goes through LDS.
 __global__ __launch_bounds__(256) void pq_transpose_codes_kernel(const uint8_t* __restrict__ codesT, int64_t n, int M,
                                                                  uint8_t* __restrict__ codes) {
@@ -1253,11 +1613,28 @@ hipError_t launch_pq_encode_cs_v(const float* x, int64_t n, int d, int M, int ds
     const int64_t chunks = pick_chunks(n, d, M, cus);
     const int64_t R = align_up(ceil_div(n, chunks), (int64_t)32);
     const int64_t grid = ceil_div(n, R) * M;
+    // V & (1 << 20): the round-1 resolve (pair window in the pair kernel, separate full-item
+    // and pair kernels), kept for A/B profiling
+    constexpr bool legacy = (V & (1 << 20)) != 0;
+    const float2* pdw = legacy ? nullptr : static_cast<const float2*>(pd);
     hipLaunchKernelGGL(kern, dim3((unsigned)grid), dim3(kThreads), smem, st, x, n, d, M, dsub, R, C, cn,
                        static_cast<const half8*>(img), hinit, static_cast<const float4*>(bnd), codesT,
-                       static_cast<uint2*>(items), static_cast<int2*>(counts), static_cast<float2*>(pinfo));
+                       static_cast<uint2*>(items), static_cast<int2*>(counts), static_cast<float2*>(pinfo), pdw,
+                       static_cast<const float4*>(bnd2));
     e = hipGetLastError();
     if (e != hipSuccess || ((V & 1) && !(V & 512))) return e;
+    if constexpr (!legacy) {
+        constexpr int msmem = merged_smem_bytes<KS>();
+        static_assert(msmem <= 160 * 1024, "merged resolve LDS");
+        auto mkern = (KS == 6 && dsub == 96) ? pq_resolve_merged_kernel<KS, (KS == 6 ? 96 : 0), V>
+                                             : pq_resolve_merged_kernel<KS, 0, V>;
+        e = hipFuncSetAttribute((const void*)mkern, hipFuncAttributeMaxDynamicSharedMemorySize, msmem);
+        if (e != hipSuccess) return e;
+        hipLaunchKernelGGL(mkern, dim3((unsigned)grid), dim3(kMWaves * 64), msmem, st, x, n, d, M, dsub, R, C, cn,
+                           static_cast<const half8*>(img), hinit, static_cast<const float4*>(bnd), codesT,
+                           static_cast<const uint2*>(items), static_cast<const int2*>(counts));
+        return hipGetLastError();
+    }
     // full items through pq_resolve_full_kernel (filter re-run + candidate chains): 1.5-2 %
     // faster end to end than the pair kernel's 256-wide scans (interleaved A/B, 1M x 1536);
     // V&256 restores the scans

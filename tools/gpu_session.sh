@@ -26,7 +26,7 @@ for s in "$@"; do
         smoke)   step smoke 400 python -c "import __graft_entry__ as g; g.smoke()" ;;
         pytest)  step pytest 900 python -m pytest tests -m gpu -q -rf ;;
         bench)   step bench 600 python bench.py --steps 10 --warmup 3 ;;
-        prof)    step prof 600 rocprofv3 --kernel-trace --stats -d $OUT/prof -o run --output-format csv -- python bench.py --steps 5 --warmup 2 --no-cpu-baseline ;;
+        prof)    step prof 600 rocprofv3 --kernel-trace --stats -d $OUT/prof -o run --output-format csv -- python bench.py --steps 5 --warmup 2 --no-cpu-baseline --no-configs --no-config5 ;;
         *)       step "custom$i" 600 bash -c "$s" ;;
     esac
 done

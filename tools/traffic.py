@@ -11,7 +11,7 @@ import sys
 from collections import defaultdict
 from pathlib import Path
 
-KERNELS = ("pq_encode_cs_kernel", "pq_resolve_full", "pq_resolve_cs_kernel", "pq_transpose_codes")
+KERNELS = ("pq_encode_cs_kernel", "pq_resolve_merged", "pq_transpose_codes")
 
 
 def per_launch(root, sub, last_n):

@@ -1210,9 +1210,16 @@ __global__ __launch_bounds__(kFWaves * 64) __attribute__((amdgpu_waves_per_eu(2)
 //   pair batch (32 rows): lane (r, 0) runs the chain of k1, lane (r, 1) that of k2; merge.
 constexpr int kMWaves = 4;
 
+// The LDS codebook keeps rows 16*KS floats apart (no room for padding) with the 16-B chunks of
+// row k permuted by j -> j ^ (k & 7) (k & 3 when a row has 4 (mod 8) chunks): random-k chain
+// reads then spread over the bank row (unswizzled, a 96-float pitch maps every row to the same
+// two bank offsets: 22 M conflict cycles per 1M-row call, PMC).
+template <int KS>
+__device__ __forceinline__ int cswz(int k) { return (4 * KS) % 8 == 0 ? (k & 7) : (k & 3); }
+
 template <int KS>
 constexpr int merged_smem_bytes() {
-    return 256 * (16 * KS) * 4 + 2 * 256 * 4 + 16 + kMWaves * (32 * (16 * KS + 4) * 4 + 64 * (kLCap + 1) * 4);
+    return 256 * 16 * KS * 4 + 2 * 256 * 4 + 16 + kMWaves * (32 * (16 * KS + 4) * 4 + 64 * kLCap * 4);
 }
 
 // V (profiling, tools/cs_variants.hip): 1 << 21 skips the full batches, 1 << 22 the pair
@@ -1230,16 +1237,19 @@ __global__ __launch_bounds__(kMWaves * 64) __attribute__((amdgpu_waves_per_eu(1,
     constexpr int FR = 8 * KS * 64;
     const int dsub = DS > 0 ? DS : dsub_in;
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-    float* cl = reinterpret_cast<float*>(smem);  // [256][DP]
-    float* cnl = cl + 256 * DP;
+    constexpr int CP = DP;
+    float* cl = reinterpret_cast<float*>(smem);  // [256][DP], chunks swizzled (cswz)
+    float* cnl = cl + 256 * CP;
     float* hb = cnl + 256;
     int* ctr = reinterpret_cast<int*>(hb + 256);
     const int tid = threadIdx.x;
     const int w = __builtin_amdgcn_readfirstlane(tid >> 6), l = tid & 63;
     const int r = l & 31, h = l >> 5;
     float* xf = reinterpret_cast<float*>(reinterpret_cast<unsigned char*>(ctr + 4) +
-                                         w * (32 * XP * 4 + 64 * (kLCap + 1) * 4));
-    int* cand = reinterpret_cast<int*>(xf + 32 * XP) + l * (kLCap + 1);  // this lane's list + a sink slot
+                                         w * (32 * XP * 4 + 64 * kLCap * 4));
+    int* cand = reinterpret_cast<int*>(xf + 32 * XP) + l * kLCap;  // this lane's candidate list
+    // its sink slot: a pad column of its staged row (never read as data)
+    int* sink = reinterpret_cast<int*>(xf + r * XP + 16 * KS + h);
 
     int m;
     int64_t chunk;
@@ -1266,7 +1276,8 @@ __global__ __launch_bounds__(kMWaves * 64) __attribute__((amdgpu_waves_per_eu(1,
 #pragma unroll
             for (int u = 0; u < 8; ++u) {
                 const int e = e0 + u * kMWaves * 64;
-                if (e < tot) *reinterpret_cast<f32x4*>(cl + 4 * e) = v[u];
+                const int k = e / q4, j = e - k * q4;
+                if (e < tot) *reinterpret_cast<f32x4*>(cl + k * CP + 4 * (j ^ cswz<KS>(k))) = v[u];
             }
         }
         cnl[tid] = cn[(int64_t)m * 256 + tid];
@@ -1289,10 +1300,11 @@ __global__ __launch_bounds__(kMWaves * 64) __attribute__((amdgpu_waves_per_eu(1,
     // centroid row is read first, then the sequential fmaf chain runs without waits)
     constexpr int NQ = DS > 0 ? DS / 4 : 1;
     auto exact_reg = [&](const f32x4 (&xv)[NQ], int k) __attribute__((always_inline)) {
-        const float* c = cl + k * DP;
+        const float* c = cl + k * CP;
+        const int sw = cswz<KS>(k);
         f32x4 cv[NQ];
 #pragma unroll
-        for (int t = 0; t < NQ; ++t) cv[t] = *reinterpret_cast<const f32x4*>(c + 4 * t);
+        for (int t = 0; t < NQ; ++t) cv[t] = *reinterpret_cast<const f32x4*>(c + 4 * (t ^ sw));
         float dot = 0.0f;
 #pragma unroll
         for (int t = 0; t < NQ; ++t) {
@@ -1309,11 +1321,12 @@ __global__ __launch_bounds__(kMWaves * 64) __attribute__((amdgpu_waves_per_eu(1,
     };
     // canonical score of centroid k for the staged row xr (sequential fmaf chain over t), any dsub
     auto exact = [&](const float* xr, int k) __attribute__((always_inline)) {
-        const float* c = cl + k * DP;
+        const float* c = cl + k * CP;
+        const int sw = cswz<KS>(k);
         float dot = 0.0f;
 #pragma unroll 2
         for (int t = 0; t < (DS > 0 ? DS : dsub); t += 4) {
-            const f32x4 cv = *reinterpret_cast<const f32x4*>(c + t);
+            const f32x4 cv = *reinterpret_cast<const f32x4*>(c + 4 * ((t >> 2) ^ sw));
             const f32x4 xv = *reinterpret_cast<const f32x4*>(xr + t);
             dot = __builtin_fmaf(xv.x, cv.x, dot);
             dot = __builtin_fmaf(xv.y, cv.y, dot);
@@ -1430,7 +1443,7 @@ __global__ __launch_bounds__(kMWaves * 64) __attribute__((amdgpu_waves_per_eu(1,
 #pragma unroll
                 for (int i = 0; i < 16; ++i) {
                     const bool in = acc[cb][i] >= thr;
-                    cand[in ? min(nc, kLCap - 1) : kLCap] = cb * 32 + (i & 3) + 8 * (i >> 2) + 4 * h;
+                    *(in ? cand + min(nc, kLCap - 1) : sink) = cb * 32 + (i & 3) + 8 * (i >> 2) + 4 * h;
                     nc += in ? 1 : 0;
                 }
             }

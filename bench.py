@@ -562,9 +562,9 @@ def main():
                        "data": a.data, "parallelism": f"row-sharded x{world}"},
             "roofline": {"bound": "hbm", "achieved": enc["achieved_gbs"], "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": frac, "traffic": traffic_from_profile(tkey),
-                         "kernel": "mivq_pq_encode call: pq_encode_cs_kernel (filter) + pq_resolve_full2_kernel and "
-                                   "pq_resolve_cs_kernel (exact re-check of the row-subspaces the filter could not "
-                                   "settle) + pq_transpose_codes16_kernel",
+                         "kernel": "mivq_pq_encode call: pq_encode_cs_kernel (fp16-MFMA filter + pair window) + "
+                                   "pq_resolve_merged_kernel (canonical fp32 re-check of the row-subspaces the filter "
+                                   "could not settle) + pq_transpose_codes16_kernel",
                          "bytes_per_vector": enc["bytes_per_vector"], "kernel_ms": enc["kernel_ms"]},
             "cpu_baseline": cpu,
             "parity_sample": parity,

@@ -17,10 +17,11 @@
 //    below the fp32 accumulation rounding every GEMM has (tests/test_opq_gpu.py checks
 //    1e-5 of ||x|| ||a|| against fp64).  Three v_mfma_f32_32x32x16_f16 per 32x32x16 block
 //    = 3 x 1/16 of the fp32-MFMA cost per flop (2.5 PF f16 vs 157 TF fp32 dense peaks).
-//    Tile: 128 x 128 outputs per 256-thread workgroup, 64 x 64 (2 x 2 MFMA blocks) per
-//    wave, K in steps of 32 staged through LDS (hi and lo planes of x and B, 80-B rows:
-//    conflict-free ds_read_b128 fragment reads), double-buffered with the next step's
-//    global loads in registers while the current step computes.  XCD-aware tile order:
+//    Tile: 256 x 256 outputs per 512-thread workgroup (8 waves of 64 x 128 = 2 x 4 MFMA
+//    blocks; 128 x 128 / 4 waves for narrow matrices), K in steps of 32 staged through LDS
+//    (hi and lo planes of x and B, 80-B rows: conflict-free ds_read_b128 fragment reads),
+//    double-buffered (160 KiB) with the next step's global loads in registers while the
+//    current step computes.  XCD-aware tile order:
 //    the workgroups one XCD runs cover consecutive tiles, so the column tiles of one row
 //    block run back to back on the same L2 (x read once from HBM).
 //    mivq_opq_prepare builds the hi / lo images of B = op(A) once per matrix ([col][k]
@@ -111,12 +112,22 @@ __global__ __launch_bounds__(256) void opq_gemm_kernel(const float* __restrict__
 }
 
 // ------------------------------------------------------------------ split-f16 kernel
-constexpr int SBM = 128, SBN = 128, SBK = 32;
+constexpr int SBK = 32;
 constexpr int SPITCH = SBK * 2 + 16;          // bytes per LDS row (64 B of halves + 16 B pad)
-constexpr int SPLANE = 128 * SPITCH;          // one 128-row plane (hi or lo of x or of B)
-constexpr int SBUF = 4 * SPLANE;              // x hi, x lo, B hi, B lo
-constexpr int kSplitSmem = 2 * SBUF;          // double-buffered: 80 KiB
 constexpr int kScaleShift = 14;               // largest |v| scaled into [2^13, 2^14]
+
+// Tile geometry: WR x WC waves, each RB x CB blocks of 32 x 32 outputs; the workgroup tile is
+// TM = 32 WR RB rows by TN = 32 WC CB columns.
+template <int WR, int WC, int RB, int CB>
+struct SplitTile {
+    static constexpr int NT = WR * WC * 64;
+    static constexpr int TM = 32 * WR * RB, TN = 32 * WC * CB;
+    static constexpr int BUF = 2 * (TM + TN) * SPITCH;  // x hi, x lo, B hi, B lo planes
+    static constexpr int SMEM = 2 * BUF;                // double-buffered
+    static_assert(TM * SBK / 4 == 4 * NT && 2 * TN * SBK / 8 == 4 * NT, "4 loads of each kind per thread");
+};
+using TileS = SplitTile<2, 2, 2, 2>;  // 128 x 128, 256 threads, 80 KiB (two per CU)
+using TileL = SplitTile<4, 2, 2, 4>;  // 256 x 256, 512 threads, 160 KiB (half the L2 traffic per MFMA)
 
 // Power-of-two scale 2^(14 - E) with max|v| = m 2^E, m in [0.5, 1); 1 for 0 / inf / NaN.
 // Clamped to fp32's normal exponents (rows below 2^-112 lose relative accuracy).
@@ -202,26 +213,30 @@ __device__ __forceinline__ int64_t xcd_tile(int64_t b, int64_t G) {
     return x * q + min(x, r) + j;
 }
 
-__global__ __launch_bounds__(256) void opq_split_gemm_kernel(const float* __restrict__ x, int64_t n, int d,
-                                                             const float* __restrict__ rs,
-                                                             const _Float16* __restrict__ bimg,
-                                                             const float* __restrict__ hdr, float* __restrict__ y,
-                                                             int64_t ctiles) {
+template <int WR, int WC, int RB, int CB>
+__global__ __launch_bounds__(WR * WC * 64) void opq_split_gemm_kernel(const float* __restrict__ x, int64_t n, int d,
+                                                                      const float* __restrict__ rs,
+                                                                      const _Float16* __restrict__ bimg,
+                                                                      const float* __restrict__ hdr,
+                                                                      float* __restrict__ y, int64_t ctiles) {
+    using T = SplitTile<WR, WC, RB, CB>;
+    constexpr int NT = T::NT, TM = T::TM, TN = T::TN;
+    constexpr int XPL = TM * SPITCH, BPL = TN * SPITCH;  // plane sizes
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     const int tid = threadIdx.x, l = tid & 63, w = tid >> 6;
-    const int wr = w >> 1, wc = w & 1;
+    const int wr = w / WC, wc = w % WC;
     const int64_t t = xcd_tile(blockIdx.x, gridDim.x);
-    const int64_t r0 = (t / ctiles) * SBM;
-    const int c0 = (int)(t % ctiles) * SBN;
+    const int64_t r0 = (t / ctiles) * TM;
+    const int c0 = (int)(t % ctiles) * TN;
     const int64_t dd = (int64_t)d * d;
 
     // staging geometry: x: 4 float4 per thread (row e / 8, k 4 (e % 8)); B: 4 x 16 B per
-    // thread (plane e / 512, col (e % 512) / 4, k 8 (e % 4))
+    // thread (plane e / (4 TN), column (e % 4 TN) / 4, k 8 (e % 4))
     float sx[4];
     int xrow[4], xk[4];
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
-        const int e = tid + 256 * u;
+        const int e = tid + NT * u;
         xrow[u] = e >> 3;
         xk[u] = 4 * (e & 7);
         const int64_t gr = r0 + xrow[u];
@@ -230,9 +245,9 @@ __global__ __launch_bounds__(256) void opq_split_gemm_kernel(const float* __rest
     int bpl[4], bcol[4], bk[4];
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
-        const int e = tid + 256 * u;
-        bpl[u] = e >> 9;
-        bcol[u] = (e & 511) >> 2;
+        const int e = tid + NT * u;
+        bpl[u] = e / (4 * TN);
+        bcol[u] = (e % (4 * TN)) >> 2;
         bk[u] = 8 * (e & 3);
     }
     float4 xv[4];
@@ -262,16 +277,16 @@ __global__ __launch_bounds__(256) void opq_split_gemm_kernel(const float* __rest
             }
             const int off = xrow[u] * SPITCH + 2 * xk[u];
             *reinterpret_cast<half4*>(buf + off) = h;
-            *reinterpret_cast<half4*>(buf + SPLANE + off) = lo;
-            *reinterpret_cast<uint4*>(buf + (2 + bpl[u]) * SPLANE + bcol[u] * SPITCH + 2 * bk[u]) = bv[u];
+            *reinterpret_cast<half4*>(buf + XPL + off) = lo;
+            *reinterpret_cast<uint4*>(buf + 2 * XPL + bpl[u] * BPL + bcol[u] * SPITCH + 2 * bk[u]) = bv[u];
         }
     };
 
-    floatx16 acc[2][2];
+    floatx16 acc[RB][CB];
 #pragma unroll
-    for (int a = 0; a < 2; ++a)
+    for (int a = 0; a < RB; ++a)
 #pragma unroll
-        for (int b = 0; b < 2; ++b)
+        for (int b = 0; b < CB; ++b)
 #pragma unroll
             for (int e = 0; e < 16; ++e) acc[a][b][e] = 0.0f;
 
@@ -281,54 +296,71 @@ __global__ __launch_bounds__(256) void opq_split_gemm_kernel(const float* __rest
     __syncthreads();
     const int fr = l & 31, fk = 16 * (l >> 5);  // fragment row / col and byte offset of its k-group
     for (int s = 0; s < nsteps; ++s) {
-        unsigned char* cur = smem + (s & 1) * SBUF;
+        unsigned char* cur = smem + (s & 1) * T::BUF;
         if (s + 1 < nsteps) gload((s + 1) * SBK);
 #pragma unroll
         for (int kk = 0; kk < 2; ++kk) {
-            half8 ah[2], al[2], bh[2], bl[2];
+            half8 ah[RB], al[RB], bh[CB], bl[CB];
 #pragma unroll
-            for (int i = 0; i < 2; ++i) {
-                const int ar = (wr * 64 + i * 32 + fr) * SPITCH + 32 * kk + fk;
-                const int bc = (wc * 64 + i * 32 + fr) * SPITCH + 32 * kk + fk;
+            for (int i = 0; i < RB; ++i) {
+                const int ar = (wr * RB * 32 + i * 32 + fr) * SPITCH + 32 * kk + fk;
                 ah[i] = *reinterpret_cast<const half8*>(cur + ar);
-                al[i] = *reinterpret_cast<const half8*>(cur + SPLANE + ar);
-                bh[i] = *reinterpret_cast<const half8*>(cur + 2 * SPLANE + bc);
-                bl[i] = *reinterpret_cast<const half8*>(cur + 3 * SPLANE + bc);
+                al[i] = *reinterpret_cast<const half8*>(cur + XPL + ar);
             }
-            // small terms first; four independent accumulators between dependent MFMAs
 #pragma unroll
-            for (int a = 0; a < 2; ++a)
+            for (int j = 0; j < CB; ++j) {
+                const int bc = (wc * CB * 32 + j * 32 + fr) * SPITCH + 32 * kk + fk;
+                bh[j] = *reinterpret_cast<const half8*>(cur + 2 * XPL + bc);
+                bl[j] = *reinterpret_cast<const half8*>(cur + 2 * XPL + BPL + bc);
+            }
+            // small terms first; RB * CB independent accumulators between dependent MFMAs
 #pragma unroll
-                for (int b = 0; b < 2; ++b) acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x16_f16(al[a], bh[b], acc[a][b], 0, 0, 0);
+            for (int a = 0; a < RB; ++a)
 #pragma unroll
-            for (int a = 0; a < 2; ++a)
+                for (int b = 0; b < CB; ++b) acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x16_f16(al[a], bh[b], acc[a][b], 0, 0, 0);
 #pragma unroll
-                for (int b = 0; b < 2; ++b) acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[a], bl[b], acc[a][b], 0, 0, 0);
+            for (int a = 0; a < RB; ++a)
 #pragma unroll
-            for (int a = 0; a < 2; ++a)
+                for (int b = 0; b < CB; ++b) acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[a], bl[b], acc[a][b], 0, 0, 0);
 #pragma unroll
-                for (int b = 0; b < 2; ++b) acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[a], bh[b], acc[a][b], 0, 0, 0);
+            for (int a = 0; a < RB; ++a)
+#pragma unroll
+                for (int b = 0; b < CB; ++b) acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[a], bh[b], acc[a][b], 0, 0, 0);
         }
-        if (s + 1 < nsteps) sstore(smem + ((s + 1) & 1) * SBUF);
+        if (s + 1 < nsteps) sstore(smem + ((s + 1) & 1) * T::BUF);
         __syncthreads();
     }
     // epilogue: undo the scales (powers of two: exact) and store
     const float binv = hdr[1];
 #pragma unroll
-    for (int a = 0; a < 2; ++a) {
+    for (int a = 0; a < RB; ++a) {
 #pragma unroll
         for (int e = 0; e < 16; ++e) {
-            const int row = wr * 64 + a * 32 + (e & 3) + 8 * (e >> 2) + 4 * (l >> 5);
+            const int row = wr * RB * 32 + a * 32 + (e & 3) + 8 * (e >> 2) + 4 * (l >> 5);
             const int64_t gr = r0 + row;
             if (gr >= n) continue;
             const float inv = binv / rs[gr];
 #pragma unroll
-            for (int b = 0; b < 2; ++b) {
-                const int gc = c0 + wc * 64 + b * 32 + (l & 31);
+            for (int b = 0; b < CB; ++b) {
+                const int gc = c0 + wc * CB * 32 + b * 32 + (l & 31);
                 if (gc < d) y[gr * d + gc] = acc[a][b][e] * inv;
             }
         }
     }
+}
+
+template <class T, int WR, int WC, int RB, int CB>
+int launch_split(const float* x, int64_t n, int d, const float* rs, const _Float16* bimg, const float* hdr, float* y,
+                 hipStream_t st) {
+    static_assert(T::SMEM <= 160 * 1024, "LDS");
+    auto kern = opq_split_gemm_kernel<WR, WC, RB, CB>;
+    hipError_t e = hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, T::SMEM);
+    if (e != hipSuccess) return set_error(MIVQ_ERR_HIP, "opq_split_gemm: %s", hipGetErrorString(e));
+    const int64_t ct = ceil_div(d, T::TN), tiles = ceil_div(n, T::TM) * ct;
+    MIVQ_REQUIRE(tiles < ((int64_t)1 << 31), MIVQ_ERR_UNSUPPORTED, "opq_rotate_prepared: n=%lld too large for one call",
+                 (long long)n);
+    hipLaunchKernelGGL(kern, dim3((unsigned)tiles), dim3(T::NT), T::SMEM, st, x, n, d, rs, bimg, hdr, y, ct);
+    return check_launch("opq_split_gemm");
 }
 
 size_t prep_bytes(int32_t d) { return 256 + (size_t)2 * d * d * sizeof(_Float16); }
@@ -390,14 +422,8 @@ extern "C" int mivq_opq_rotate_prepared(const float* x, int64_t n, int32_t d, co
     hipLaunchKernelGGL(opq_row_scale_kernel, dim3((unsigned)ceil_div(n, 4)), dim3(256), 0, st, x, n, d, rs);
     int rc = check_launch("opq_row_scale");
     if (rc) return rc;
-    static_assert(kSplitSmem <= 160 * 1024, "LDS");
-    hipError_t e = hipFuncSetAttribute((const void*)opq_split_gemm_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                       kSplitSmem);
-    if (e != hipSuccess) return set_error(MIVQ_ERR_HIP, "opq_split_gemm: %s", hipGetErrorString(e));
-    const int64_t ct = ceil_div(d, SBN), tiles = ceil_div(n, SBM) * ct;
-    MIVQ_REQUIRE(tiles < ((int64_t)1 << 31), MIVQ_ERR_UNSUPPORTED, "opq_rotate_prepared: n=%lld too large for one call",
-                 (long long)n);
-    hipLaunchKernelGGL(opq_split_gemm_kernel, dim3((unsigned)tiles), dim3(256), kSplitSmem, st, x, n, d, rs, bimg, hdr,
-                       y, ct);
-    return check_launch("opq_split_gemm");
+    // 256 x 256 tiles (512 threads, 160 KiB) wherever a row block spans at least one such
+    // tile; the 128 x 128 kernel for narrow matrices
+    if (d >= 256 && n >= 256) return launch_split<TileL, 4, 2, 2, 4>(x, n, d, rs, bimg, hdr, y, st);
+    return launch_split<TileS, 2, 2, 2, 2>(x, n, d, rs, bimg, hdr, y, st);
 }

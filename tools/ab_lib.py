@@ -1,0 +1,97 @@
+"""Interleaved A/B of mivq_pq_encode between two builds of libmivq.so (same process, same data).
+
+usage: python tools/ab_lib.py OTHER.so [--n 1000000] [--d 1536] [--M 16] [--data gaussian] [--reps 10]
+The in-tree library (vector-quantization_amd/lib/libmivq.so) is "this"; OTHER.so is e.g. a
+build of the previous commit (git stash; make; cp lib/libmivq.so /tmp/old.so; git stash pop).
+Prints per-call medians of alternating single calls (HIP events) and back-to-back rates, and
+checks that both builds emit identical codes.
+"""
+import argparse
+import ctypes
+import sys
+from pathlib import Path
+
+import torch
+
+ROOT = Path(__file__).resolve().parent.parent
+sys.path.insert(0, str(ROOT / "vector-quantization_amd"))
+sys.path.insert(0, str(ROOT))
+from haag_vq import _native  # noqa: E402
+from haag_vq.methods._kmeans import train_pq  # noqa: E402
+from bench import synth  # noqa: E402
+
+
+def bind(path):
+    lib = ctypes.CDLL(str(path))
+    for name, (res, args) in _native.SIGNATURES.items():
+        if hasattr(lib, name):
+            f = getattr(lib, name)
+            f.restype, f.argtypes = res, args
+    return lib
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("other")
+    ap.add_argument("--n", type=int, default=1_000_000)
+    ap.add_argument("--d", type=int, default=1536)
+    ap.add_argument("--M", type=int, default=16)
+    ap.add_argument("--data", default="gaussian")
+    ap.add_argument("--reps", type=int, default=10)
+    a = ap.parse_args()
+    dev = _native.require_device()
+    libs = {"this": bind(_native.LIB_PATH), "other": bind(a.other if Path(a.other).is_absolute() else ROOT / a.other)}
+    X = synth(a.n, a.d, 0, dev, kind=a.data)
+    C = train_pq(X[:65536], a.M, 8, niter=25, seed=1234).contiguous()
+    st = torch.cuda.current_stream().cuda_stream
+    P = ctypes.c_void_p
+    state = {}
+    for k, lb in libs.items():
+        prep = torch.empty(lb.mivq_pq_prep_bytes(a.d, a.M, 8), dtype=torch.uint8, device=dev)
+        assert lb.mivq_pq_prepare(P(C.data_ptr()), a.d, a.M, 8, P(prep.data_ptr()), P(st)) == 0
+        nb = lb.mivq_pq_encode_workspace_bytes(a.n, a.d, a.M, 8)
+        ws = torch.empty(nb, dtype=torch.uint8, device=dev)
+        out = torch.empty((a.n, a.M), dtype=torch.uint8, device=dev)
+        state[k] = (prep, ws, out)
+
+    def run(k):
+        lb = libs[k]
+        prep, ws, out = state[k]
+        rc = lb.mivq_pq_encode(P(X.data_ptr()), a.n, a.d, a.M, 8, P(C.data_ptr()), P(prep.data_ptr()),
+                               P(ws.data_ptr()), ws.numel(), P(out.data_ptr()), 0, P(st))
+        assert rc == 0, rc
+
+    for k in libs:
+        run(k)
+    torch.cuda.synchronize()
+    same = bool(torch.equal(state["this"][2], state["other"][2]))
+    print(f"codes identical: {same}", flush=True)
+    res = {k: [] for k in libs}
+    for _ in range(a.reps * 3):
+        for k in libs:
+            s_, e_ = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            s_.record(); run(k); e_.record()
+            torch.cuda.synchronize()
+            res[k].append(s_.elapsed_time(e_))
+    for k in libs:
+        t = sorted(res[k])
+        print(f"AB {k}: median {t[len(t) // 2]:.3f} ms  min {t[0]:.3f}  max {t[-1]:.3f}", flush=True)
+    for rnd in range(2):
+        for k in libs:
+            s_, e_ = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            for _ in range(3):
+                run(k)
+            s_.record()
+            for _ in range(20):
+                run(k)
+            e_.record()
+            torch.cuda.synchronize()
+            ms = s_.elapsed_time(e_) / 20
+            gbs = a.n * (4 * a.d + a.M) / (ms * 1e-3) / 1e9
+            print(f"AB {k} round {rnd}: back-to-back {ms:.3f} ms/call = {gbs / 8000:.3f} of 8 TB/s", flush=True)
+    if not same:
+        sys.exit(1)
+
+
+if __name__ == "__main__":
+    main()

@@ -452,7 +452,8 @@ __global__ __launch_bounds__(kThreads) void pq_encode_cs_kernel(
             top3_insert(t1, t2, t3, p3);
         }
         // Xs >= ||sigma x||: |sigma x - x~| <= 2^-11 |sigma x| + 2^-24 per component
-        const float Xs = (sqrtf(xx) * (1.0f + 1e-5f) + xs_eta) * (1.0f + 9.765625e-4f);
+        // (v_sqrt_f32: 1 ulp, inside the 1e-5 margin; a flushed denormal xx still leaves Xs >= xs_eta)
+        const float Xs = (__builtin_amdgcn_sqrtf(xx) * (1.0f + 1e-5f) + xs_eta) * (1.0f + 9.765625e-4f);
         const float W = bm.y * Xs + bm.z;
         const float thr = t1 - W;
         const bool bad = !(Xs < 65000.0f) || !isfinite(t1) || !isfinite(W);
@@ -934,7 +935,7 @@ __global__ __launch_bounds__(kFWaves * 64) void pq_resolve_full_kernel(
 #pragma unroll
             for (int i = 0; i < 16; ++i) t1 = fmaxf(t1, acc[cb][i]);
         t1 = fmaxf(t1, __shfl_xor(t1, 32));
-        const float Xs = (sqrtf(xx) * (1.0f + 1e-5f) + xs_eta) * (1.0f + 9.765625e-4f);
+        const float Xs = (__builtin_amdgcn_sqrtf(xx) * (1.0f + 1e-5f) + xs_eta) * (1.0f + 9.765625e-4f);
         const float W = bm.y * Xs + bm.z;
         const float thr = t1 - W;
         const bool bad = !(Xs < 65000.0f) || !isfinite(t1) || !isfinite(W);
@@ -1123,7 +1124,7 @@ __global__ __launch_bounds__(kFWaves * 64) __attribute__((amdgpu_waves_per_eu(2)
             for (int i = 0; i < 16; ++i) t1 = fmaxf(t1, acc[i]);
         }
         t1 = fmaxf(t1, __shfl_xor(t1, 32));
-        const float Xs = (sqrtf(xx) * (1.0f + 1e-5f) + xs_eta) * (1.0f + 9.765625e-4f);
+        const float Xs = (__builtin_amdgcn_sqrtf(xx) * (1.0f + 1e-5f) + xs_eta) * (1.0f + 9.765625e-4f);
         const float W = bm.y * Xs + bm.z;
         const float thr = t1 - W;
         const bool bad = !(Xs < 65000.0f) || !isfinite(t1) || !isfinite(W);
@@ -1426,7 +1427,7 @@ __global__ __launch_bounds__(kMWaves * 64) __attribute__((amdgpu_waves_per_eu(1,
 #pragma unroll
                 for (int i = 0; i < 16; ++i) t1 = fmaxf(t1, acc[cb][i]);
             t1 = fmaxf(t1, __shfl_xor(t1, 32));
-            const float Xs = (sqrtf(xx) * (1.0f + 1e-5f) + xs_eta) * (1.0f + 9.765625e-4f);
+            const float Xs = (__builtin_amdgcn_sqrtf(xx) * (1.0f + 1e-5f) + xs_eta) * (1.0f + 9.765625e-4f);
             const float W = bm.y * Xs + bm.z;
             const float thr = t1 - W;
             const bool bad = !(Xs < 65000.0f) || !isfinite(t1) || !isfinite(W);

@@ -116,6 +116,9 @@ __device__ __forceinline__ void lut_add(const float* tab, uint32_t mk, float (&d
     }
 }
 
+typedef float f32x4v __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(3))) const f32x4v lds_f4;
+
 // Undoes the odd lanes' half order of lut_add<8> (identity for other QB).
 template <int QB>
 __device__ __forceinline__ void lut_unswap(float (&dist)[QB], uint32_t par) {
@@ -131,11 +134,18 @@ __device__ __forceinline__ void lut_unswap(float (&dist)[QB], uint32_t par) {
 
 // grid (nchunks, ceil(nq / QB)), block kScanWaves waves sharing the QB LUTs in LDS (so the
 // CU keeps 4 waves per SIMD despite the 128 KiB of tables).  Part index = chunk*kScanWaves + wave.
-template <int R, int QB>
+// MC > 0 (M = 16 MC, ksub = 256, 16-B aligned code rows): each lane's row of codes is MC
+// 16-B loads issued one wave-step ahead, so the LDS lookups never wait on the code fetch
+// (MC = 0: 4-B code words loaded in the step that uses them).
+template <int R, int QB, int MC>
 __global__ __launch_bounds__(kScanWaves * 64) void adc_scan_kernel(
     const float* __restrict__ lut, int64_t nq, const uint8_t* __restrict__ codes, int64_t n, int M,
     int ksub, int k, int64_t id_offset, int64_t chunk_rows, float* __restrict__ part_d,
     uint32_t* __restrict__ part_i) {
+    if constexpr (MC > 0) {
+        M = 16 * MC;
+        ksub = 256;
+    }
     // [M][ksub][QB]: the QB queries' entries of one (m, code) are adjacent, so one 16-B LDS
     // read serves 4 queries (random codes: ~2x fewer bank-conflict cycles per lookup than
     // QB separate 4-B reads)
@@ -165,13 +175,67 @@ __global__ __launch_bounds__(kScanWaves * 64) void adc_scan_kernel(
     const int64_t rend = min(n, rbeg + chunk_rows);
     const bool words = (M % 4) == 0;
     const uint32_t par = (uint32_t)lane & 1u;
+    const uint32_t tbase = (uint32_t)(uintptr_t)tab + 16u * par;  // LDS byte address of the half read first
+    uint4 cw[MC > 0 ? MC : 1];
+    auto fetch = [&](int64_t row) __attribute__((always_inline)) {
+        if constexpr (MC > 0) {
+            const uint4* cr = reinterpret_cast<const uint4*>(codes + row * (16 * MC));
+#pragma unroll
+            for (int c = 0; c < MC; ++c) cw[c] = row < rend ? cr[c] : make_uint4(0u, 0u, 0u, 0u);
+        }
+    };
+    fetch(rbeg + (int64_t)wv * 64 + lane);
     for (int64_t base = rbeg + (int64_t)wv * 64; base < rend; base += kScanWaves * 64) {
         const int64_t row = base + lane;
         const bool valid = row < rend;
         float dist[QB];
 #pragma unroll
         for (int qq = 0; qq < QB; ++qq) dist[qq] = 0.0f;
-        if (valid) {
+        if constexpr (MC > 0) {
+            uint4 cur[MC];
+#pragma unroll
+            for (int c = 0; c < MC; ++c) cur[c] = cw[c];
+            fetch(row + kScanWaves * 64);
+            // one word (4 sub-codes) per iteration, the queue of words rotating through
+            // registers (a rolled loop: unrolled, the 16 MC lookups' reads and addresses
+            // outgrow the 128 registers of the 16-wave workgroup)
+            uint32_t wq[4 * MC];
+#pragma unroll
+            for (int c = 0; c < MC; ++c) {
+                wq[4 * c + 0] = cur[c].x; wq[4 * c + 1] = cur[c].y;
+                wq[4 * c + 2] = cur[c].z; wq[4 * c + 3] = cur[c].w;
+            }
+#pragma unroll 1
+            for (int jw = 0; jw < 4 * MC; ++jw) {
+                const uint32_t wrd = wq[0];
+                if constexpr (QB == 8) {
+                    // byte offsets: group (4 jw + b, code) at 32 (256 (4 jw + b) + code); the half
+                    // read first at +16 par, the other at that ^ 16; the b term (a multiple of 32)
+                    // goes to the instruction's offset field: 3 VALU per lookup for addresses
+                    const uint32_t wofs = tbase + (uint32_t)jw * (4u * 256u * 32u);
+#pragma unroll
+                    for (int b = 0; b < 4; ++b) {
+                        // inline asm keeps the three ops as written (left to itself the compiler
+                        // re-derives o2 from the pieces with more adds)
+                        uint32_t cb, o1, o2;
+                        asm("v_bfe_u32 %0, %1, %2, 8" : "=v"(cb) : "v"(wrd), "i"(8 * b));
+                        asm("v_lshl_add_u32 %0, %1, 5, %2" : "=v"(o1) : "v"(cb), "v"(wofs));
+                        asm("v_xor_b32 %0, 16, %1" : "=v"(o2) : "v"(o1));
+                        const f32x4v t0 = *(reinterpret_cast<const lds_f4*>((uintptr_t)o1) + b * 512);
+                        const f32x4v t1 = *(reinterpret_cast<const lds_f4*>((uintptr_t)o2) + b * 512);
+                        dist[0] += t0.x; dist[1] += t0.y; dist[2] += t0.z; dist[3] += t0.w;
+                        dist[4] += t1.x; dist[5] += t1.y; dist[6] += t1.z; dist[7] += t1.w;
+                    }
+                } else {
+#pragma unroll
+                    for (int b = 0; b < 4; ++b)
+                        lut_add<QB>(tab, (uint32_t)((4 * jw + b) * 256) + ((wrd >> (8 * b)) & 0xFFu), dist, par);
+                }
+#pragma unroll
+                for (int t = 0; t + 1 < 4 * MC; ++t) wq[t] = wq[t + 1];
+            }
+            lut_unswap<QB>(dist, par);
+        } else if (valid) {
             const uint8_t* cr = codes + row * M;
             if (words) {
                 for (int m0 = 0; m0 < M; m0 += 4) {
@@ -395,7 +459,9 @@ template <int R, int QB>
 hipError_t launch_scan(const float* lut, int64_t nq, const uint8_t* codes, int64_t n, int M, int ksub, int k,
                        int64_t id_offset, int64_t nch, float* pd, uint32_t* pi, hipStream_t st) {
     const size_t smem = (size_t)QB * M * ksub * sizeof(float);
-    auto kern = adc_scan_kernel<R, QB>;
+    const bool vec = ksub == 256 && reinterpret_cast<uintptr_t>(codes) % 16 == 0;
+    auto kern = vec && M == 16 ? adc_scan_kernel<R, QB, 1> : vec && M == 32 ? adc_scan_kernel<R, QB, 2>
+                                                                             : adc_scan_kernel<R, QB, 0>;
     hipError_t e = hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);
     if (e != hipSuccess) return e;
     const int64_t chunk_rows = ceil_div(n, nch);

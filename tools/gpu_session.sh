@@ -24,8 +24,9 @@ for s in "$@"; do
     i=$((i+1))
     case "$s" in
         smoke)   step smoke 400 python -c "import __graft_entry__ as g; g.smoke()" ;;
-        pytest)  step pytest 900 python -m pytest tests -m gpu -q -rf ;;
+        pytest)  step pytest 900 python -u -m pytest tests -m gpu -q -rf --timeout 120 --timeout-method thread ;;
         bench)   step bench 600 python bench.py --steps 10 --warmup 3 ;;
+        bench10m) step bench10m 600 python bench.py --n 10000000 --steps 5 --warmup 2 --no-adc --no-cpu-baseline --no-alt-data --no-config5 --no-configs ;;
         prof)    step prof 600 rocprofv3 --kernel-trace --stats -d $OUT/prof -o run --output-format csv -- python bench.py --steps 5 --warmup 2 --no-cpu-baseline --no-configs --no-config5 ;;
         *)       step "custom$i" 600 bash -c "$s" ;;
     esac

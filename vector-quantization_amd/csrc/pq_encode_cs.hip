@@ -178,7 +178,6 @@ constexpr int max_loads() {
     return (32 + (16 / KS) - 1) / (16 / KS);
 }
 
-constexpr int kLCap = 8;  // candidates per lane (128 centroids); more -> the lane scans all of them
 
 // V: profiling variants (tools/cs_variants.hip), 0 in the library.  Bits drop work and
 // produce wrong codes: 1 the resolve kernel, 2 its full scans, 4 its pair checks, 8 its x
@@ -1198,17 +1197,21 @@ __global__ __launch_bounds__(kFWaves * 64) __attribute__((amdgpu_waves_per_eu(2)
 // pairs its filter could not settle with the pair window.  One workgroup (4 waves, one per
 // SIMD: up to 512 registers per lane) per encode workgroup; LDS holds the exact fp32 codebook
 // C_m (the canonical chains of both kinds read it), the norms, the accumulator init, and per
-// wave a 32-row fp32 staging tile plus a candidate list.  A full batch loads the filter's f16 A
-// operands of all 8 centroid blocks (192 registers at KS = 6, from the L2-resident prepared
-// image) together with its row gather.
+// wave a 32-row fp32 staging tile.  A full batch loads the filter's f16 A operands of all 8
+// centroid blocks (192 registers at KS = 6, from the L2-resident prepared image) together with
+// its row gather.
 //   full batch (32 rows): gather the rows, build the B operand exactly as the filter does, one
-//     MFMA sweep with all 8 accumulators kept, t1 = max, every centroid inside the window
-//     (score >= t1 - W) goes to the row's candidate list; the two lanes of a row then run the
-//     canonical chains of alternate candidates and merge (s, k).  Every minimiser of the
-//     canonical score lies inside the window, so the smallest (s, k) is the canonical code.
-//     Rows the window cannot vouch for (non-finite, out of range) or with more than kFCap
-//     candidates are scanned over all 256 centroids.
+//     MFMA sweep with all 8 accumulators kept, t1 = max; each lane marks its centroids inside
+//     the window (score >= t1 - W) in a 128-bit mask (registers only) and runs their canonical
+//     chains in increasing k, one loop for all of them; the two lanes of a row merge (s, k).
+//     Every minimiser of the canonical score lies inside the window, so the smallest (s, k) is
+//     the canonical code.  Rows the window cannot vouch for (non-finite, out of range) take all
+//     256 centroids.  (Round 1 appended the candidates to per-lane LDS lists: 128 conflicted
+//     stores per lane per batch.)
 //   pair batch (32 rows): lane (r, 0) runs the chain of k1, lane (r, 1) that of k2; merge.
+// (Measured and dropped: claiming batches one ahead so the next pair batch's rows load during
+// the current one, 4 -> 1 fewer exposed gathers per batch but +10 % per launch: the gathers are
+// HBM-bound at ~4 TB/s of random 384-B segments, not latency-bound.)
 constexpr int kMWaves = 4;
 
 // The LDS codebook keeps rows 16*KS floats apart (no room for padding) with the 16-B chunks of
@@ -1220,7 +1223,7 @@ __device__ __forceinline__ int cswz(int k) { return (4 * KS) % 8 == 0 ? (k & 7) 
 
 template <int KS>
 constexpr int merged_smem_bytes() {
-    return 256 * 16 * KS * 4 + 2 * 256 * 4 + 16 + kMWaves * (32 * (16 * KS + 4) * 4 + 64 * kLCap * 4);
+    return 256 * 16 * KS * 4 + 2 * 256 * 4 + 16 + kMWaves * (32 * (16 * KS + 4) * 4);
 }
 
 // V (profiling, tools/cs_variants.hip): 1 << 21 skips the full batches, 1 << 22 the pair
@@ -1247,10 +1250,7 @@ __global__ __launch_bounds__(kMWaves * 64) __attribute__((amdgpu_waves_per_eu(1,
     const int w = __builtin_amdgcn_readfirstlane(tid >> 6), l = tid & 63;
     const int r = l & 31, h = l >> 5;
     float* xf = reinterpret_cast<float*>(reinterpret_cast<unsigned char*>(ctr + 4) +
-                                         w * (32 * XP * 4 + 64 * kLCap * 4));
-    int* cand = reinterpret_cast<int*>(xf + 32 * XP) + l * kLCap;  // this lane's candidate list
-    // its sink slot: a pad column of its staged row (never read as data)
-    int* sink = reinterpret_cast<int*>(xf + r * XP + 16 * KS + h);
+                                         w * (32 * XP * 4));
 
     int m;
     int64_t chunk;
@@ -1436,45 +1436,39 @@ __global__ __launch_bounds__(kMWaves * 64) __attribute__((amdgpu_waves_per_eu(1,
                 lds_fence();
                 continue;
             }
-            // this lane's centroids inside the window, appended without branches (the slot
-            // after the list is a sink); the lane then runs their canonical chains
-            int nc = 0;
+            // this lane's centroids inside the window as a 128-bit mask (4 words of two centroid
+            // blocks; register-only, no per-value LDS stores), then their canonical chains in
+            // increasing k, one loop for all of them; a row the window cannot vouch for takes
+            // all 128 of the lane's centroids
+            uint32_t wm[4];
 #pragma unroll
-            for (int cb = 0; cb < 8; ++cb) {
+            for (int q2 = 0; q2 < 4; ++q2) {
+                uint32_t mm = 0u;
 #pragma unroll
-                for (int i = 0; i < 16; ++i) {
-                    const bool in = acc[cb][i] >= thr;
-                    *(in ? cand + min(nc, kLCap - 1) : sink) = cb * 32 + (i & 3) + 8 * (i >> 2) + 4 * h;
-                    nc += in ? 1 : 0;
-                }
+                for (int i = 0; i < 32; ++i) mm |= acc[2 * q2 + (i >> 4)][i & 15] >= thr ? (1u << i) : 0u;
+                wm[q2] = bad ? 0xFFFFFFFFu : mm;
             }
-            lds_fence();
             float bs = INFINITY;
             int bk = 256;
             auto take = [&](float sc, int k) __attribute__((always_inline)) {
                 if (sc < bs || (sc == bs && k < bk)) { bs = sc; bk = k; }
             };
             if (r < cntb && !(V & (1 << 24))) {
-                if (bad || nc > kLCap) {
-                    // the lane's 128 centroids, increasing k
-                    for (int cb = 0; cb < 8; ++cb)
-                        for (int qq = 0; qq < 4; ++qq)
-                            for (int e = 0; e < 4; ++e) {
-                                const int k = cb * 32 + 8 * qq + 4 * h + e;
-                                take(exact(xr, k), k);
-                            }
-                } else if constexpr (DS > 0) {
-                    f32x4 xv[NQ];
-                    load_row(xr, xv);
-                    for (int j = 0; j < nc; ++j) {
-                        const int k = cand[j];
-                        take(exact_reg(xv, k), k);
-                    }
-                } else {
-                    for (int j = 0; j < nc; ++j) {
-                        const int k = cand[j];
-                        take(exact(xr, k), k);
-                    }
+                f32x4 xv[NQ];
+                if constexpr (DS > 0) load_row(xr, xv);
+                while ((wm[0] | wm[1] | wm[2] | wm[3]) != 0u) {
+                    const int wi = wm[0] ? 0 : wm[1] ? 1 : wm[2] ? 2 : 3;
+                    const uint32_t wsel = wm[0] ? wm[0] : wm[1] ? wm[1] : wm[2] ? wm[2] : wm[3];
+                    const int bit = __builtin_ctz(wsel);
+                    const uint32_t rest = wsel & (wsel - 1u);
+                    wm[0] = wi == 0 ? rest : wm[0];
+                    wm[1] = wi == 1 ? rest : wm[1];
+                    wm[2] = wi == 2 ? rest : wm[2];
+                    wm[3] = wi == 3 ? rest : wm[3];
+                    const int cb = 2 * wi + (bit >> 4), i = bit & 15;
+                    const int k = cb * 32 + (i & 3) + 8 * (i >> 2) + 4 * h;
+                    if constexpr (DS > 0) take(exact_reg(xv, k), k);
+                    else take(exact(xr, k), k);
                 }
             }
             const float os = __shfl_xor(bs, 32);

@@ -1209,9 +1209,9 @@ __global__ __launch_bounds__(kFWaves * 64) __attribute__((amdgpu_waves_per_eu(2)
 //     256 centroids.  (Round 1 appended the candidates to per-lane LDS lists: 128 conflicted
 //     stores per lane per batch.)
 //   pair batch (32 rows): lane (r, 0) runs the chain of k1, lane (r, 1) that of k2; merge.
-// (Measured and dropped: claiming batches one ahead so the next pair batch's rows load during
-// the current one, 4 -> 1 fewer exposed gathers per batch but +10 % per launch: the gathers are
-// HBM-bound at ~4 TB/s of random 384-B segments, not latency-bound.)
+// (Tried and dropped: claiming batches one ahead so the next pair batch's rows load during the
+// current one: no gain (+10 % per launch in that build).  With every chain and MFMA skipped the
+// launch still takes ~85 us: the row gathers run at ~4 TB/s of random 384-B segments.)
 constexpr int kMWaves = 4;
 
 // The LDS codebook keeps rows 16*KS floats apart (no room for padding) with the 16-B chunks of

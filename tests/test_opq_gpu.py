@@ -35,7 +35,7 @@ def _check(y, X, B):
     assert not np.isfinite(y[~fin]).all(axis=1).any()
 
 
-@pytest.mark.parametrize("n,d", [(1000, 1536), (777, 1024), (300, 776), (65, 8), (1, 64)])
+@pytest.mark.parametrize("n,d", [(1000, 1536), (777, 1024), (400, 288), (300, 776), (65, 8), (1, 64)])
 @pytest.mark.parametrize("transpose", [False, True])
 def test_split_gemm_vs_fp64(dev, n, d, transpose):
     from haag_vq import _native
@@ -54,6 +54,21 @@ def test_split_gemm_vs_fp64(dev, n, d, transpose):
     assert prep is not None
     y = _native.opq_rotate_prepared(_t(X, dev), prep).cpu().numpy()
     _check(y, X, A if transpose else A.T)
+
+
+def test_split_gemm_chunk_boundary(dev):
+    """More rows than one GEMM chunk (2^20 rows: the f16 planes of x are built per chunk):
+    rows on both sides of the boundary and the ragged end match fp64."""
+    from haag_vq import _native
+
+    n, d = (1 << 20) + 300, 256
+    g = torch.Generator(device=dev).manual_seed(7)
+    X = torch.randn((n, d), device=dev, generator=g)
+    A = _orth(d, 11)
+    prep = _native.opq_prepare(_t(A, dev), False)
+    y = _native.opq_rotate_prepared(X, prep)
+    for lo, hi in ((0, 200), ((1 << 20) - 200, (1 << 20) + 200), (n - 100, n)):
+        _check(y[lo:hi].cpu().numpy(), X[lo:hi].cpu().numpy(), A.T)
 
 
 @pytest.mark.parametrize("n,d", [(500, 1536), (130, 100)])

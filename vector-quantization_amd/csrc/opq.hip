@@ -7,27 +7,25 @@
 //
 // Two kernels:
 //
-// 1. opq_split_gemm_kernel (mivq_opq_rotate_prepared, the product path): fp32-accurate
-//    GEMM out of f16 MFMAs.  Every operand is split into two f16 terms, v = hi + lo with
-//    hi = f16(s v), lo = f16(s v - hi) (the difference is exact in fp32), after a
-//    power-of-two scale s that puts the largest |v| of the row (x) or of the matrix (A) at
-//    2^13..2^14, inside f16's range.  y = (x_hi b_hi + x_hi b_lo + x_lo b_hi) / (s_x s_b):
-//    each f16 x f16 product is exact in the fp32 accumulator, and the terms left out
-//    (x_lo b_lo and the residuals of the two splits) are <= ~3 * 2^-22 of |x_k b_k|, far
-//    below the fp32 accumulation rounding every GEMM has (tests/test_opq_gpu.py checks
-//    1e-5 of ||x|| ||a|| against fp64).  Three v_mfma_f32_32x32x16_f16 per 32x32x16 block
-//    = 3 x 1/16 of the fp32-MFMA cost per flop (2.5 PF f16 vs 157 TF fp32 dense peaks).
-//    Tile: 256 x 256 outputs per 512-thread workgroup (8 waves of 64 x 128 = 2 x 4 MFMA
-//    blocks; 128 x 128 / 4 waves for narrow matrices), K in steps of 32 staged through LDS
-//    (hi and lo planes of x and B, 80-B rows: conflict-free ds_read_b128 fragment reads),
-//    double-buffered (160 KiB) with the next step's global loads in registers while the
-//    current step computes.  XCD-aware tile order:
-//    the workgroups one XCD runs cover consecutive tiles, so the column tiles of one row
-//    block run back to back on the same L2 (x read once from HBM).
-//    mivq_opq_prepare builds the hi / lo images of B = op(A) once per matrix ([col][k]
-//    rows, scaled); mivq_opq_rotate_prepared computes the row scales of x (one pass) and
-//    runs the GEMM.
-//
+// 1. mivq_opq_rotate_prepared (the product path): fp32-accurate GEMM out of f16 MFMAs.
+//    Every operand is split into two f16 terms, v = hi + lo with hi = f16(s v),
+//    lo = f16(s v - hi) (the difference is exact in fp32), after a power-of-two scale s that
+//    puts the largest |v| of the row (x) or of the matrix (A) at 2^13..2^14, inside f16's
+//    range.  y = (x_hi b_hi + x_hi b_lo + x_lo b_hi) / (s_x s_b): each f16 x f16 product is
+//    exact in the fp32 accumulator, and the terms left out (x_lo b_lo and the residuals of the
+//    two splits) are <= ~3 * 2^-22 of |x_k b_k|, far below the fp32 accumulation rounding every
+//    GEMM has (tests/test_opq_gpu.py checks 1e-5 of ||x|| ||a|| against fp64).  Three
+//    v_mfma_f32_32x32x16_f16 per 32x32x16 block = 3 x 1/16 of the fp32-MFMA cost per flop.
+//    mivq_opq_prepare builds the hi / lo images of B = op(A) once per matrix ([col][k] rows,
+//    scaled).  d % 32 == 0 (the shapes that matter): opq_split_x_kernel writes x's row scales
+//    and hi / lo planes (one pass, chunks of 2^20 rows in the workspace), then
+//    opq_glds_gemm_kernel: 256 x 256 tiles per 512-thread workgroup (8 waves of 64 x 128 =
+//    2 x 4 MFMA blocks), all four planes global -> LDS by global_load_lds_dwordx4 (no register
+//    staging, chunk-swizzled unpadded rows: conflict-free fragment reads), two 64-KiB stages.
+//    Other d: opq_row_scale_kernel + opq_split_gemm_kernel, which splits x itself while staging
+//    (register-staged, 80-B padded rows, 256 x 256 or 128 x 128 tiles).  Both: XCD-aware tile
+//    order (the workgroups one XCD runs cover consecutive tiles, so the column tiles of a row
+//    block share its L2) and an epilogue that goes out through LDS as 16-B row stores.
 // 2. opq_gemm_kernel (mivq_opq_rotate, no preparation, any d): plain fp32 MFMA
 //    (v_mfma_f32_32x32x2_f32), 128 x 128 tiles, BK = 16 slices staged through LDS.
 #include <math.h>
@@ -163,6 +161,45 @@ __global__ __launch_bounds__(256) void opq_row_scale_kernel(const float* __restr
     if (l == 0) rs[row] = bad ? 1.0f : pow2_scale(m);
 }
 
+// Row scale and split of x in one pass (one wave per row): rs[row] = s_x, and the f16 planes
+// xs[0][row][k] = hi, xs[1][row][k] = lo of s_x x[row][k] (the GEMM then stages them by plain
+// 16-B copies instead of re-splitting x once per column tile).
+__global__ __launch_bounds__(256) void opq_split_x_kernel(const float* __restrict__ x, int64_t n, int d,
+                                                          float* __restrict__ rs, _Float16* __restrict__ xs) {
+    const int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    const int l = threadIdx.x & 63;
+    if (row >= n) return;
+    const float4* xr = reinterpret_cast<const float4*>(x + row * d);
+    const int q = d >> 2;  // d % 8 == 0
+    float m = 0.0f;
+    bool bad = false;
+    for (int k = l; k < q; k += 64) {
+        const float4 v = xr[k];
+        bad |= !isfinite(v.x) || !isfinite(v.y) || !isfinite(v.z) || !isfinite(v.w);
+        m = fmaxf(m, fmaxf(fmaxf(fabsf(v.x), fabsf(v.y)), fmaxf(fabsf(v.z), fabsf(v.w))));
+    }
+    for (int o = 32; o > 0; o >>= 1) m = fmaxf(m, __shfl_xor(m, o));
+    bad = __any(bad);
+    const float s = bad ? 1.0f : pow2_scale(m);
+    if (l == 0) rs[row] = s;
+    half4* ph = reinterpret_cast<half4*>(xs + row * d);
+    half4* pl = reinterpret_cast<half4*>(xs + (n + row) * d);
+    for (int k = l; k < q; k += 64) {
+        const float4 v = xr[k];
+        const float w[4] = {v.x * s, v.y * s, v.z * s, v.w * s};
+        half4 h, lo;
+#pragma unroll
+        for (int t = 0; t < 4; ++t) {
+            _Float16 a, b;
+            split2(w[t], a, b);
+            h[t] = a;
+            lo[t] = b;
+        }
+        ph[k] = h;
+        pl[k] = lo;
+    }
+}
+
 // max |A| over the whole matrix -> header {s_b, 1 / s_b} of the prepared image (one workgroup).
 __global__ __launch_bounds__(1024) void opq_absmax_kernel(const float* __restrict__ A, int64_t cnt,
                                                           float* __restrict__ hdr) {
@@ -211,6 +248,43 @@ __global__ __launch_bounds__(256) void opq_split_b_kernel(const float* __restric
 __device__ __forceinline__ int64_t xcd_tile(int64_t b, int64_t G) {
     const int64_t x = b & 7, j = b >> 3, q = G >> 3, r = G & 7;
     return x * q + min(x, r) + j;
+}
+
+// Epilogue of both split GEMMs: y = acc / (s_x s_b) (powers of two: exact).  The wave's
+// RB x CB blocks go out half a wave tile (32 rows) at a time through its own LDS slice
+// (32 x 32 CB floats, the staging buffers being dead by then): accumulator layout in, rows of
+// 16-B stores out (one 64-bit address per row instead of per element, no per-element
+// bounds branches, one row-scale load per lane).  Callers pass the block after a barrier.
+template <int RB, int CB>
+__device__ __forceinline__ void store_tile(const floatx16 (&acc)[RB][CB], unsigned char* smem, int w, int l,
+                                           int64_t rowbase, int colbase, int64_t n, int d,
+                                           const float* __restrict__ rs, float binv, float* __restrict__ y) {
+    constexpr int CW = CB * 32, LPR = CW / 4, RPIT = 64 / LPR;
+    float* tw = reinterpret_cast<float*>(smem) + w * 32 * CW;
+#pragma unroll
+    for (int a = 0; a < RB; ++a) {
+        const int64_t gra = rowbase + a * 32 + (l & 31);
+        const float rsl = rs[gra < n ? gra : n - 1];
+#pragma unroll
+        for (int b = 0; b < CB; ++b)
+#pragma unroll
+            for (int e = 0; e < 16; ++e)
+                tw[((e & 3) + 8 * (e >> 2) + 4 * (l >> 5)) * CW + b * 32 + (l & 31)] = acc[a][b][e];
+        __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): the wave's own slice
+        __builtin_amdgcn_wave_barrier();
+#pragma unroll
+        for (int it = 0; it < 32 / RPIT; ++it) {
+            const int rl = it * RPIT + l / LPR, cl = 4 * (l % LPR);
+            const float4 v = *reinterpret_cast<const float4*>(tw + rl * CW + cl);
+            const float sc = binv / __shfl(rsl, rl);
+            const int64_t gr = rowbase + a * 32 + rl;
+            const int gc = colbase + cl;
+            if (gr < n && gc < d)  // d % 8 == 0: the whole float4 is inside the row
+                *reinterpret_cast<float4*>(y + gr * d + gc) = make_float4(v.x * sc, v.y * sc, v.z * sc, v.w * sc);
+        }
+        __builtin_amdgcn_s_waitcnt(0xC07F);
+        __builtin_amdgcn_wave_barrier();
+    }
 }
 
 template <int WR, int WC, int RB, int CB>
@@ -330,23 +404,151 @@ __global__ __launch_bounds__(WR * WC * 64) void opq_split_gemm_kernel(const floa
         if (s + 1 < nsteps) sstore(smem + ((s + 1) & 1) * T::BUF);
         __syncthreads();
     }
-    // epilogue: undo the scales (powers of two: exact) and store
-    const float binv = hdr[1];
+    // epilogue (the staging buffers are reused: every wave must be done with them)
+    __syncthreads();
+    store_tile<RB, CB>(acc, smem, w, l, r0 + wr * RB * 32, c0 + wc * CB * 32, n, d, rs, hdr[1], y);
+}
+
+// LDS-DMA variant (x pre-split): all four planes (x hi, x lo, B hi, B lo) go global -> LDS
+// with global_load_lds_dwordx4, no register staging.  One wave-instruction writes 1 KiB of one
+// plane contiguously (the LDS destination is lane-linear), so the planes are unpadded rows of
+// 2 KSTEP bytes whose 16-B chunks are permuted through the SOURCE address (64-B rows:
+// c ^ ((r >> 2) & 3); 32-B rows: c ^ ((r >> 3) & 1)): the rows one 16-lane group of a fragment
+// ds_read_b128 touches then land on 16 distinct chunk slots of the bank row.
+// NS stages in a ring: the loads run NS - 1 K steps ahead; each step waits (counted vmcnt) for
+// its own stage only, then one raw s_barrier both publishes it and retires the slot the next
+// load overwrites (no __syncthreads: its fence would drain every load in flight).
+template <int KSTEP, int NS>
+struct GldsCfg {
+    static constexpr int ROWB = 2 * KSTEP;          // bytes per plane row
+    static constexpr int PL = 256 * ROWB;           // one plane of one stage
+    static constexpr int STAGE = 4 * PL;            // x hi, x lo, B hi, B lo
+    static constexpr int SMEM = NS * STAGE;
+    static constexpr int CPR = ROWB / 16;           // 16-B chunks per row
+    static constexpr int RPI = 64 / CPR;            // rows per DMA instruction
+    static constexpr int IPW = STAGE / 1024 / 8;    // DMA instructions per wave per stage
+    static_assert(SMEM <= 160 * 1024 && IPW * (NS - 1) <= 60, "glds ring");
+};
+
+template <int ROWB>
+__device__ __forceinline__ int glds_swz(int row) { return ROWB == 64 ? ((row >> 2) & 3) : ((row >> 3) & 1); }
+
+typedef __attribute__((address_space(3))) void lds_void;
+
+template <int KSTEP, int NS>
+__global__ __launch_bounds__(512) void opq_glds_gemm_kernel(int64_t n, int d, const _Float16* __restrict__ xsp,
+                                                            const float* __restrict__ rs,
+                                                            const _Float16* __restrict__ bimg,
+                                                            const float* __restrict__ hdr, float* __restrict__ y,
+                                                            int64_t ctiles) {
+    using G = GldsCfg<KSTEP, NS>;
+    constexpr int WC = 2, RB = 2, CB = 4, TM = 256, TN = 256;
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    const int tid = threadIdx.x, l = tid & 63, w = tid >> 6;
+    const int wr = w / WC, wc = w % WC;
+    const int64_t t = xcd_tile(blockIdx.x, gridDim.x);
+    const int64_t r0 = (t / ctiles) * TM;
+    const int c0 = (int)(t % ctiles) * TN;
+    const int64_t dd = (int64_t)d * d;
+
+    // this lane's source for each of the wave's IPW DMA instructions per stage: instruction
+    // q = IPW w + i covers plane q / (PL / 1024), rows RPI (q % (PL / 1024)) + [0, RPI); lane l
+    // -> row + l / CPR, physical chunk l % CPR holding logical chunk (l % CPR) ^ swz(row).
+    // Rows past n / columns past d read row n - 1 / column d - 1 (their outputs are dropped).
+    constexpr int QPP = G::PL / 1024;  // instructions per plane
+    const _Float16* src[G::IPW];
 #pragma unroll
-    for (int a = 0; a < RB; ++a) {
-#pragma unroll
-        for (int e = 0; e < 16; ++e) {
-            const int row = wr * RB * 32 + a * 32 + (e & 3) + 8 * (e >> 2) + 4 * (l >> 5);
-            const int64_t gr = r0 + row;
-            if (gr >= n) continue;
-            const float inv = binv / rs[gr];
-#pragma unroll
-            for (int b = 0; b < CB; ++b) {
-                const int gc = c0 + wc * CB * 32 + b * 32 + (l & 31);
-                if (gc < d) y[gr * d + gc] = acc[a][b][e] * inv;
-            }
+    for (int i = 0; i < G::IPW; ++i) {
+        const int q = G::IPW * w + i, pl = q / QPP;
+        const int row = G::RPI * (q % QPP) + l / G::CPR;
+        const int c = (l % G::CPR) ^ glds_swz<G::ROWB>(row);
+        if (pl < 2) {
+            const int64_t gr = min(r0 + row, n - 1);
+            src[i] = xsp + ((int64_t)pl * n + gr) * d + 8 * c;
+        } else {
+            const int64_t gc = min((int64_t)c0 + row, (int64_t)d - 1);
+            src[i] = bimg + (int64_t)(pl - 2) * dd + gc * d + 8 * c;
         }
     }
+    auto issue = [&](int step, int slot) __attribute__((always_inline)) {
+#pragma unroll
+        for (int i = 0; i < G::IPW; ++i) {
+            const int q = G::IPW * w + i;
+            lds_void* dst = (lds_void*)(smem + slot * G::STAGE + (q / QPP) * G::PL + (q % QPP) * 1024);
+            __builtin_amdgcn_global_load_lds((const void*)(src[i] + step * KSTEP), dst, 16, 0, 0);
+        }
+    };
+
+    floatx16 acc[RB][CB];
+#pragma unroll
+    for (int a = 0; a < RB; ++a)
+#pragma unroll
+        for (int b = 0; b < CB; ++b)
+#pragma unroll
+            for (int e = 0; e < 16; ++e) acc[a][b][e] = 0.0f;
+
+    const int fr = l & 31, fh = l >> 5;
+    auto frag = [&](const unsigned char* plane, int row, int kk) __attribute__((always_inline)) {
+        const int c = (2 * kk + fh) ^ glds_swz<G::ROWB>(row);
+        return *reinterpret_cast<const half8*>(plane + row * G::ROWB + 16 * c);
+    };
+    const int nsteps = d / KSTEP;
+#pragma unroll
+    for (int st = 0; st < NS - 1; ++st)
+        if (st < nsteps) issue(st, st);
+    for (int s = 0; s < nsteps; ++s) {
+        // stage s landed: the loads issued after it (steps s + 1 .. s + NS - 2) may stay in flight
+        if (nsteps - 1 - s >= NS - 2) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(G::IPW * (NS - 2)) : "memory");
+        else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();
+        if (s + NS - 1 < nsteps) issue(s + NS - 1, (s + NS - 1) % NS);
+        const unsigned char* cur = smem + (s % NS) * G::STAGE;
+#pragma unroll
+        for (int kk = 0; kk < KSTEP / 16; ++kk) {
+            half8 ah[RB], al[RB], bh[CB], bl[CB];
+#pragma unroll
+            for (int i = 0; i < RB; ++i) {
+                const int row = wr * RB * 32 + i * 32 + fr;
+                ah[i] = frag(cur, row, kk);
+                al[i] = frag(cur + G::PL, row, kk);
+            }
+#pragma unroll
+            for (int j = 0; j < CB; ++j) {
+                const int row = wc * CB * 32 + j * 32 + fr;
+                bh[j] = frag(cur + 2 * G::PL, row, kk);
+                bl[j] = frag(cur + 3 * G::PL, row, kk);
+            }
+#pragma unroll
+            for (int a = 0; a < RB; ++a)
+#pragma unroll
+                for (int b = 0; b < CB; ++b) acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x16_f16(al[a], bh[b], acc[a][b], 0, 0, 0);
+#pragma unroll
+            for (int a = 0; a < RB; ++a)
+#pragma unroll
+                for (int b = 0; b < CB; ++b) acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[a], bl[b], acc[a][b], 0, 0, 0);
+#pragma unroll
+            for (int a = 0; a < RB; ++a)
+#pragma unroll
+                for (int b = 0; b < CB; ++b) acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[a], bh[b], acc[a][b], 0, 0, 0);
+        }
+    }
+    // epilogue (the staging buffers are reused: every wave must be done with them)
+    __syncthreads();
+    store_tile<RB, CB>(acc, smem, w, l, r0 + wr * RB * 32, c0 + wc * CB * 32, n, d, rs, hdr[1], y);
+}
+
+template <int KSTEP, int NS>
+int launch_glds(const _Float16* xsp, int64_t n, int d, const float* rs, const _Float16* bimg, const float* hdr,
+                float* y, hipStream_t st) {
+    using G = GldsCfg<KSTEP, NS>;
+    auto kern = opq_glds_gemm_kernel<KSTEP, NS>;
+    hipError_t e = hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, G::SMEM);
+    if (e != hipSuccess) return set_error(MIVQ_ERR_HIP, "opq_glds_gemm: %s", hipGetErrorString(e));
+    const int64_t ct = ceil_div(d, 256), tiles = ceil_div(n, 256) * ct;
+    MIVQ_REQUIRE(tiles < ((int64_t)1 << 31), MIVQ_ERR_UNSUPPORTED, "opq_rotate_prepared: n=%lld too large for one call",
+                 (long long)n);
+    hipLaunchKernelGGL(kern, dim3((unsigned)tiles), dim3(512), G::SMEM, st, n, d, xsp, rs, bimg, hdr, y, ct);
+    return check_launch("opq_glds_gemm");
 }
 
 template <class T, int WR, int WC, int RB, int CB>
@@ -399,9 +601,13 @@ extern "C" int mivq_opq_prepare(const float* A, int32_t d, int32_t transpose, vo
     return check_launch("opq_split_b");
 }
 
+// Rows per GEMM launch: the f16 planes of x (4 B per element) live in the workspace for one
+// chunk at a time.
+constexpr int64_t kOpqChunk = (int64_t)1 << 20;
+
 extern "C" size_t mivq_opq_rotate_workspace_bytes(int64_t n, int32_t d) {
-    (void)d;
-    return n > 0 ? align_up((size_t)n * sizeof(float), 256) : 0;
+    if (n <= 0 || d <= 0) return 0;
+    return align_up((size_t)n * sizeof(float), 256) + align_up((size_t)std::min(n, kOpqChunk) * d * 4, 256);
 }
 
 extern "C" int mivq_opq_rotate_prepared(const float* x, int64_t n, int32_t d, const void* prep, void* workspace,
@@ -415,15 +621,39 @@ extern "C" int mivq_opq_rotate_prepared(const float* x, int64_t n, int32_t d, co
     const size_t need = mivq_opq_rotate_workspace_bytes(n, d);
     MIVQ_REQUIRE(workspace && workspace_bytes >= need, MIVQ_ERR_WORKSPACE, "opq_rotate_prepared: workspace %zu < %zu",
                  workspace_bytes, need);
+    MIVQ_REQUIRE(reinterpret_cast<uintptr_t>(workspace) % 16 == 0, MIVQ_ERR_INVALID,
+                 "opq_rotate_prepared: workspace must be 16-byte aligned");
     hipStream_t st = as_stream(stream);
     float* rs = static_cast<float*>(workspace);
+    _Float16* xsp = reinterpret_cast<_Float16*>(static_cast<unsigned char*>(workspace) +
+                                                align_up((size_t)n * sizeof(float), 256));
     const float* hdr = static_cast<const float*>(prep);
     const _Float16* bimg = reinterpret_cast<const _Float16*>(static_cast<const unsigned char*>(prep) + 256);
-    hipLaunchKernelGGL(opq_row_scale_kernel, dim3((unsigned)ceil_div(n, 4)), dim3(256), 0, st, x, n, d, rs);
-    int rc = check_launch("opq_row_scale");
-    if (rc) return rc;
-    // 256 x 256 tiles (512 threads, 160 KiB) wherever a row block spans at least one such
-    // tile; the 128 x 128 kernel for narrow matrices
-    if (d >= 256 && n >= 256) return launch_split<TileL, 4, 2, 2, 4>(x, n, d, rs, bimg, hdr, y, st);
-    return launch_split<TileS, 2, 2, 2, 2>(x, n, d, rs, bimg, hdr, y, st);
+    // d % 32 == 0 with at least one 256 x 256 tile: x split once into its f16 planes, then the
+    // LDS-DMA GEMM; otherwise row scales only and the register-staged GEMM splits x itself
+    const bool dma = d % 32 == 0 && d >= 256;
+    for (int64_t c0 = 0; c0 < n; c0 += kOpqChunk) {
+        const int64_t cn = std::min(kOpqChunk, n - c0);
+        const float* xc = x + c0 * d;
+        float* yc = y + c0 * d;
+        int rc;
+        if (dma && cn >= 256) {
+            hipLaunchKernelGGL(opq_split_x_kernel, dim3((unsigned)ceil_div(cn, 4)), dim3(256), 0, st, xc, cn, d,
+                               rs + c0, xsp);
+            rc = check_launch("opq_split_x");
+            if (rc) return rc;
+            rc = launch_glds<32, 2>(xsp, cn, d, rs + c0, bimg, hdr, yc, st);
+        } else {
+            hipLaunchKernelGGL(opq_row_scale_kernel, dim3((unsigned)ceil_div(cn, 4)), dim3(256), 0, st, xc, cn, d,
+                               rs + c0);
+            rc = check_launch("opq_row_scale");
+            if (rc) return rc;
+            // 256 x 256 tiles (512 threads, 160 KiB) wherever a row block spans at least one
+            // such tile; the 128 x 128 kernel for narrow matrices
+            rc = (d >= 256 && cn >= 256) ? launch_split<TileL, 4, 2, 2, 4>(xc, cn, d, rs + c0, bimg, hdr, yc, st)
+                                         : launch_split<TileS, 2, 2, 2, 2>(xc, cn, d, rs + c0, bimg, hdr, yc, st);
+        }
+        if (rc) return rc;
+    }
+    return MIVQ_OK;
 }

@@ -244,6 +244,36 @@ def test_sq_golden_bit_exact(dev, golden_dir):
         np.testing.assert_array_equal(r.view(np.uint8), recon.view(np.uint8), err_msg=tag)
 
 
+@pytest.mark.parametrize("bits", [4, 8, 16])
+def test_sq_vector_path_equals_generic(dev, bits):
+    """The aligned f32 encode (column-stationary kernel) against the generic kernel (taken for
+    d % 8 != 0): the first d columns of X and of X with one extra column go through the two
+    paths with the same lo / den, and their codes must be identical, over wide magnitudes,
+    values on both sides of the data range, non-finite entries and extreme den values."""
+    from haag_vq import _native
+
+    n, d = 200_000, 64
+    g = torch.Generator(device=dev).manual_seed(bits)
+    scale = torch.logspace(-30, 30, d, device=dev)
+    X = torch.randn((n, d), device=dev, generator=g) * scale
+    X[::97, 5] = float("nan")
+    X[::89, 6] = float("inf")
+    lo = X.nan_to_num(posinf=0.0).amin(0) * 0.9
+    hi = X.nan_to_num(posinf=0.0).amax(0) * 0.9  # values beyond both ends of the range
+    den = (hi - lo) + 1e-8
+    den[7] = 3.0e36   # beyond the reciprocal range: that group divides
+    den[8] = 1.0e-35
+    Xp = torch.cat([X, torch.zeros((n, 1), device=dev)], 1).contiguous()
+    lop = torch.cat([lo, lo[:1]]).contiguous()
+    denp = torch.cat([den, den[:1]]).contiguous()
+    a = _native.sq_encode(X.contiguous(), lo.contiguous(), den.contiguous(), bits)
+    b = _native.sq_encode(Xp, lop, denp, bits)
+    if bits == 4:
+        np.testing.assert_array_equal(_h(a), _h(b)[:, : d // 2])
+    else:
+        np.testing.assert_array_equal(_h(a), _h(b)[:, :d])
+
+
 @pytest.mark.parametrize("n,d", [(500, 1024), (333, 3072), (77, 37)])
 @pytest.mark.parametrize("metric", [1, 0])
 def test_rabitq_parity(dev, oracle, n, d, metric):

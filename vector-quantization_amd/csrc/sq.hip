@@ -10,6 +10,8 @@
 //
 // Layout: one lane handles 8 consecutive dims of a row (HBM-bound; vector loads and packed
 // stores on the aligned f32 fast path).
+#include <algorithm>
+
 #include "mivq_common.h"
 
 namespace mivq {
@@ -65,26 +67,14 @@ __global__ void sq_encode_kernel(const T* __restrict__ x, int64_t n, int d, cons
     }
 }
 
-// Fast path (f32, d % 8 == 0, 16-B aligned rows): one lane per 8 dims, two 16-B loads of x,
-// lo and den, one 4 / 8 / 16-B store of the packed codes.  Same arithmetic as above.
-__global__ void sq_encode_f32_vec_kernel(const float* __restrict__ x, int64_t n, int d, const float* __restrict__ lo,
-                                         const float* __restrict__ den, int nbits, void* __restrict__ codes) {
-    const uint32_t groups = (uint32_t)(d >> 3);
-    const uint64_t gid = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (gid >= (uint64_t)n * groups) return;
-    const uint64_t i = gid / groups;
-    const int j0 = (int)(gid - i * groups) * 8;
-    const float4* xr = reinterpret_cast<const float4*>(x + i * (uint64_t)d + j0);
-    const float4* lr = reinterpret_cast<const float4*>(lo + j0);
-    const float4* dr = reinterpret_cast<const float4*>(den + j0);
-    const float4 xa = xr[0], xb = xr[1], la = lr[0], lb = lr[1], da = dr[0], db = dr[1];
-    const float L = (float)((1 << nbits) - 1);
-    const float xv[8] = {xa.x, xa.y, xa.z, xa.w, xb.x, xb.y, xb.z, xb.w};
-    const float lv[8] = {la.x, la.y, la.z, la.w, lb.x, lb.y, lb.z, lb.w};
-    const float dv[8] = {da.x, da.y, da.z, da.w, db.x, db.y, db.z, db.w};
-    uint32_t q[8];
-#pragma unroll
-    for (int u = 0; u < 8; ++u) q[u] = np_cast_uint(sq_step(xv[u], lv[u], dv[u], L));
+// Fast path (f32, d % 8 == 0, 16-B aligned rows): column-stationary.  Block (gx, gy) covers
+// column groups 64 gx + [0, 64) (8 dims each, one per lane) of rows kSqRows gy + [0, kSqRows);
+// a lane keeps its 8 lo / den values in registers and walks its rows (wave w takes rows
+// w, w + 4, ...), four rows in flight: two 16-B loads of x and one 4 / 8 / 16-B store of
+// packed codes per row, no per-element index arithmetic.  Same arithmetic as above.
+constexpr int kSqRows = 64;
+
+__device__ __forceinline__ void sq_pack_store(const uint32_t (&q)[8], int nbits, void* codes, uint64_t i, int d, int j0) {
     if (nbits == 8) {
         uint2 w;
         w.x = (q[0] & 0xFF) | (q[1] & 0xFF) << 8 | (q[2] & 0xFF) << 16 | (q[3] & 0xFF) << 24;
@@ -100,6 +90,46 @@ __global__ void sq_encode_f32_vec_kernel(const float* __restrict__ x, int64_t n,
 #pragma unroll
         for (int u = 0; u < 8; u += 2) w |= (uint32_t)(uint8_t)(((uint8_t)q[u] << 4) | (uint8_t)q[u + 1]) << (4 * u);
         *reinterpret_cast<uint32_t*>(static_cast<uint8_t*>(codes) + i * (uint64_t)(d >> 1) + (j0 >> 1)) = w;
+    }
+}
+
+__global__ __launch_bounds__(256) void sq_encode_f32_vec_kernel(const float* __restrict__ x, int64_t n, int d,
+                                                                const float* __restrict__ lo,
+                                                                const float* __restrict__ den, int nbits,
+                                                                void* __restrict__ codes) {
+    const int g = blockIdx.x * 64 + (threadIdx.x & 63);
+    if (g >= (d >> 3)) return;
+    const int j0 = 8 * g;
+    const float4 la = *reinterpret_cast<const float4*>(lo + j0), lb = *reinterpret_cast<const float4*>(lo + j0 + 4);
+    const float4 da = *reinterpret_cast<const float4*>(den + j0), db = *reinterpret_cast<const float4*>(den + j0 + 4);
+    const float lv[8] = {la.x, la.y, la.z, la.w, lb.x, lb.y, lb.z, lb.w};
+    const float dv[8] = {da.x, da.y, da.z, da.w, db.x, db.y, db.z, db.w};
+    const float L = (float)((1 << nbits) - 1);
+    for (int64_t rbk = blockIdx.y; rbk * kSqRows < n; rbk += gridDim.y) {
+    const int64_t r0 = rbk * kSqRows + (threadIdx.x >> 6);
+    const int64_t r1 = min(n, (rbk + 1) * kSqRows);
+    for (int64_t i0 = r0; i0 < r1; i0 += 16) {
+        float4 xa[4], xb[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const int64_t i = i0 + 4 * k;
+            if (i < r1) {
+                const float4* xr = reinterpret_cast<const float4*>(x + i * (uint64_t)d + j0);
+                xa[k] = xr[0];
+                xb[k] = xr[1];
+            }
+        }
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const int64_t i = i0 + 4 * k;
+            if (i >= r1) break;
+            const float xv[8] = {xa[k].x, xa[k].y, xa[k].z, xa[k].w, xb[k].x, xb[k].y, xb[k].z, xb[k].w};
+            uint32_t q[8];
+#pragma unroll
+            for (int u = 0; u < 8; ++u) q[u] = np_cast_uint(sq_step(xv[u], lv[u], dv[u], L));
+            sq_pack_store(q, nbits, codes, (uint64_t)i, d, j0);
+        }
+    }
     }
 }
 
@@ -177,7 +207,9 @@ int sq_encode(const T* x, int64_t n, int32_t d, const T* lo, const T* den, int32
                                            reinterpret_cast<uintptr_t>(den)) % 16 == 0) &&
                          (reinterpret_cast<uintptr_t>(codes) % 16 == 0);
         if (vec) {
-            hipLaunchKernelGGL(sq_encode_f32_vec_kernel, dim3((unsigned)ceil_div(work, 256)), dim3(256), 0,
+            // grid.y is limited to 65535: blocks stride over the row blocks beyond that
+            const int64_t rb = std::min<int64_t>(ceil_div(n, (int64_t)kSqRows), 65535);
+            hipLaunchKernelGGL(sq_encode_f32_vec_kernel, dim3((unsigned)ceil_div(d / 8, 64), (unsigned)rb), dim3(256), 0,
                                as_stream(stream), x, n, d, lo, den, nbits, codes);
             return check_launch(name);
         }

@@ -15,6 +15,8 @@ Second-level legs (keys of the same JSON line):
              reference's own search on the same codes (decode + exact L2), the LDS roofline
              of the scan, and (rank 0, N = 1) the oracle's ADC on the host cores.
   alt_data   the headline encode on the other synthetic distribution (clustered rows).
+  north_star (N = 1 only) the north-star size: the headline encode on 10M x 1536 Gaussian
+             rows (BASELINE north_star "10M x 1536 at 1 GPU"), parity on a 200,000-row sample.
   config5    BASELINE configs[4], the MS MARCO shape: 6.65M x 1024 rows per GPU (53.2M over
              8 GPUs), PQ16 encode + ADC top-10 of 10,000 queries with the RCCL merge.
   configs    (N = 1 only) configs[2] OPQ32 encode + ADC recall@10 (1M x 1536) and configs[3]
@@ -80,6 +82,8 @@ def parse(argv=None):
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-adc", action="store_true")
     ap.add_argument("--no-alt-data", action="store_true")
+    ap.add_argument("--no-north-star", action="store_true")
+    ap.add_argument("--north-star-rows", type=int, default=10_000_000)
     ap.add_argument("--no-config5", action="store_true")
     ap.add_argument("--no-configs", action="store_true")
     ap.add_argument("--config5-rows", type=int, default=6_650_000, help="config #5 rows per GPU")
@@ -524,6 +528,24 @@ def main():
         log(f"[rank 0] alt data: {alt}")
         del Xa, ca
 
+    ns = None
+    if head_only and not a.no_north_star and a.north_star_rows > a.n:
+        Xn = synth(a.north_star_rows, a.d, seed=11, dev=dev, kind="gaussian")
+        Cn = train_codebook(Xn, a.M, 8, 0, 1, dev)
+        cn_, en = encode_leg(Xn, Cn, a, 0, 1, dev, 3, 1)
+        pn = None
+        if not a.no_cpu_baseline:
+            pn = parity_check(Xn, Cn, cn_, _oracle(), max_rows=200_000, fp64_rows=5000)[0]
+        ns = {"workload": f"pq{a.M}_encode_{a.north_star_rows}x{a.d}", "data": "gaussian",
+              "value": a.north_star_rows / en["wall_s"], "unit": "vectors/s", "ms_per_step": en["wall_s"] * 1e3,
+              "steps": 3, "warmup": 1, "kernel_ms": en["kernel_ms"],
+              "roofline": {"bound": "hbm", "achieved": en["achieved_gbs"], "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                           "frac": en["achieved_gbs"] / HBM_PEAK_GBS, "bytes_per_vector": en["bytes_per_vector"]},
+              "parity": pn}
+        log(f"[rank 0] north star: {ns}")
+        del Xn, cn_
+        torch.cuda.empty_cache()
+
     c5 = None
     if not a.no_config5:
         c5 = config5_leg(a, rank, world, dev, a.steps, a.warmup)
@@ -570,6 +592,7 @@ def main():
             "parity_sample": parity,
             "adc": adc,
             "alt_data": alt,
+            "north_star": ns,
             "config5": c5,
             "configs": configs,
         }

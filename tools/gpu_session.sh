@@ -27,7 +27,7 @@ for s in "$@"; do
         pytest)  step pytest 900 python -u -m pytest tests -m gpu -q -rf --timeout 120 --timeout-method thread ;;
         bench)   step bench 600 python bench.py --steps 10 --warmup 3 ;;
         bench10m) step bench10m 600 python bench.py --n 10000000 --steps 5 --warmup 2 --no-adc --no-cpu-baseline --no-alt-data --no-config5 --no-configs ;;
-        prof)    step prof 600 rocprofv3 --kernel-trace --stats -d $OUT/prof -o run --output-format csv -- python bench.py --steps 5 --warmup 2 --no-cpu-baseline --no-configs --no-config5 ;;
+        prof)    step prof 600 rocprofv3 --kernel-trace --stats -d $OUT/prof -o run --output-format csv -- python bench.py --steps 5 --warmup 2 --no-cpu-baseline --no-configs --no-config5 --no-north-star ;;
         *)       step "custom$i" 600 bash -c "$s" ;;
     esac
 done

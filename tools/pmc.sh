@@ -7,7 +7,7 @@ tag=$1; shift
 OUT=gpurun_out/pmc_$tag
 mkdir -p $OUT
 rocprofv3 -L > $OUT/counters_list.txt 2>&1 || true
-BENCH="python bench.py --no-adc --no-cpu-baseline --no-alt-data --no-config5 --no-configs --steps 3 --warmup 1 $*"
+BENCH="python bench.py --no-adc --no-cpu-baseline --no-alt-data --no-north-star --no-config5 --no-configs --steps 3 --warmup 1 $*"
 i=0
 for group in \
     "FETCH_SIZE" \

@@ -1,0 +1,110 @@
+"""The header's threading contract (include/mivq.h: stream-ordered, safe to call from several
+host threads on different streams, no global mutable state besides the per-thread error
+string; SURVEY.md §8(b) "Threading"): two host threads, each on its own HIP stream, run the
+PQ encode, the prepared OPQ rotation and the ADC search on different data at the same time,
+repeatedly, and every result equals the one computed alone.  Also: an error raised in one
+thread leaves the other thread's calls and messages untouched."""
+
+import threading
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+torch = pytest.importorskip("torch")
+
+
+def _work(dev, seed):
+    from haag_vq import _native
+    from haag_vq.methods._kmeans import train_pq
+
+    g = torch.Generator(device=dev).manual_seed(seed)
+    X = torch.randn((60_000, 768), device=dev, generator=g)
+    X = X / X.norm(dim=1, keepdim=True)
+    C = train_pq(X[:8192], 8, 8, niter=4, seed=seed).contiguous()
+    A, _ = torch.linalg.qr(torch.randn((768, 768), device=dev, generator=g, dtype=torch.float64))
+    A = A.float().contiguous()
+    return X, C, A
+
+
+def _run(dev, X, C, A):
+    from haag_vq import _native
+
+    prep = _native.pq_prepare(C, 8)
+    codes = _native.pq_encode(X, C, prep, 8)
+    oprep = _native.opq_prepare(A, False)
+    Y = _native.opq_rotate_prepared(X, oprep)
+    lut = _native.adc_lut(X[:64], C, 8)
+    dists, ids = _native.adc_search(lut, codes, 10, 8)
+    return codes, Y, dists, ids
+
+
+def test_two_threads_two_streams_match_serial(dev):
+    inputs = [_work(dev, s) for s in (1, 2)]
+    torch.cuda.synchronize()
+    ref = [tuple(t.cpu() for t in _run(dev, *inp)) for inp in inputs]
+    torch.cuda.synchronize()
+
+    results = [None, None]
+    errors = []
+
+    def worker(i):
+        try:
+            s = torch.cuda.Stream(device=dev)
+            with torch.cuda.stream(s):
+                out = None
+                for _ in range(4):
+                    out = _run(dev, *inputs[i])
+                s.synchronize()
+                results[i] = tuple(t.cpu() for t in out)
+        except Exception as e:  # surfaced below
+            errors.append(repr(e))
+
+    th = [threading.Thread(target=worker, args=(i,)) for i in range(2)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join(timeout=300)
+    assert not errors, errors
+    for i in range(2):
+        for got, want in zip(results[i], ref[i]):
+            assert torch.equal(got, want), i
+
+
+def test_error_message_is_per_thread(dev):
+    """A library error in one thread (workspace too small: the C side fails and records its
+    message) while another thread encodes: the failing thread reads its own message, the other
+    thread's call succeeds and its last-error string stays empty."""
+    from haag_vq import _native
+
+    lib = _native.load_library()
+    C = torch.zeros((8, 256, 96), device=dev)
+    prep = _native.pq_prepare(C, 8)
+    X = torch.zeros((16, 768), device=dev)
+    out = torch.empty((16, 8), dtype=torch.uint8, device=dev)
+    barrier = threading.Barrier(2)
+    seen = {}
+
+    def bad():
+        barrier.wait()
+        try:
+            _native._call("mivq_pq_encode", _native._ptr(X), 16, 768, 8, 8, _native._ptr(C), _native._ptr(prep),
+                          None, 0, _native._ptr(out), 0, _native._stream())
+        except RuntimeError as e:
+            seen["bad"] = str(e)
+
+    def good():
+        barrier.wait()
+        for _ in range(20):
+            seen["good"] = _native.pq_encode(X, C, prep, 8).cpu().numpy()
+        seen["good_err"] = lib.mivq_last_error().decode()
+
+    th = [threading.Thread(target=bad), threading.Thread(target=good)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join(timeout=120)
+    assert "workspace" in seen["bad"], seen
+    np.testing.assert_array_equal(seen["good"], np.zeros((16, 8), np.uint8))
+    assert seen["good_err"] == "", seen["good_err"]

@@ -35,8 +35,9 @@ PQ_SHAPES = [
     (1000, 1536, 16, 8),    # MFMA KS=6 (the headline shape)
     (777, 1024, 16, 8),     # MFMA KS=4, ragged n
     (513, 1536, 32, 8),     # MFMA KS=3 (OPQ32 shape)
-    (300, 1024, 8, 8),      # MFMA KS=8 (dsub 128)
-    (300, 1536, 8, 8),      # dsub 192 -> exact path
+    (300, 1024, 8, 8),      # wide filter KS=8 (dsub 128, 4 waves, codebook read from L2)
+    (300, 1536, 8, 8),      # wide filter KS=12 (dsub 192: config #1's PQ8 at D=1536)
+    (300, 1120, 8, 8),      # wide filter KS=9 (dsub 140, padded K)
     (200, 48, 6, 8),        # dsub 8, KS=1
     (257, 48, 12, 8),       # dsub 4
     (256, 16, 4, 4),        # nbits 4 (faiss bit stream)

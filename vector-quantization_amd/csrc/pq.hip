@@ -724,7 +724,7 @@ extern "C" int mivq_pq_encode(const float* x, int64_t n, int32_t d, int32_t M, i
     const bool aligned = (reinterpret_cast<uintptr_t>(x) % 16 == 0) && (d % 4 == 0) && (L.dsub % 4 == 0);
     const bool exact_only = (flags_in & MIVQ_PQ_FORCE_EXACT) != 0;
     // (the code transpose after the filter stages (256 + 16) * M bytes of LDS: M <= 512)
-    const bool cs_ok = L.mfma && aligned && !exact_only && L.ks <= 6 && cs_smem_bytes(L.ks, L.dsub) <= 160 * 1024 &&
+    const bool cs_ok = L.mfma && aligned && !exact_only && L.ks <= 12 && cs_smem_bytes(L.ks, L.dsub) <= 160 * 1024 &&
                        M <= 512 && !(flags_in & MIVQ_PQ_LEGACY_MFMA);
     const bool mfma_ok = L.mfma && aligned && L.ks <= 8 && !exact_only && mfma_smem_bytes(L.ks, M) <= 160 * 1024;
     if (cs_ok) {

@@ -54,7 +54,10 @@ typedef float f32x4 __attribute__((ext_vector_type(4)));
 #endif
 constexpr int kWaves = MIVQ_CS_WAVES;  // 768 threads, 3 waves per SIMD (profiling builds may override)
 constexpr int kDepth = 1;   // x blocks in flight per wave
-constexpr int kThreads = kWaves * 64;
+// Wide subspaces (dsub 97..192, KS 7..12): the f16 image alone takes up to 96 KiB of LDS, so
+// the filter runs 4 waves (one per SIMD, up to 512 registers) with two blocks in flight each.
+constexpr int kWideWaves = 4;
+constexpr int cs_waves(int KS) { return KS <= 6 ? kWaves : kWideWaves; }
 constexpr int kRsrcWord3 = 0x00020000;  // gfx9 buffer resource: 32-bit data format
 constexpr int kXAux = 2;  // x stream cache policy: nt (read once)
 
@@ -195,8 +198,8 @@ constexpr int max_loads() {
 // workgroup into `counts`.
 // DS > 0: the kernel for sub-rows of exactly DS floats (the addresses and load counts fold
 // to constants); DS = 0 reads dsub at run time.
-template <int KS, int LAYOUT, int V = 0, int DS = 0>
-__global__ __launch_bounds__(kThreads) void pq_encode_cs_kernel(
+template <int KS, int LAYOUT, int V = 0, int DS = 0, int NW = kWaves>
+__global__ __launch_bounds__(NW * 64) void pq_encode_cs_kernel(
     const float* __restrict__ x, int64_t n, int d, int M, int dsub_in, int64_t rows_per_wg,
     const float* __restrict__ C, const float* __restrict__ cn, const half8* __restrict__ img,
     const float* __restrict__ hinit, const float4* __restrict__ bnd, uint8_t* __restrict__ codesT,
@@ -208,10 +211,12 @@ __global__ __launch_bounds__(kThreads) void pq_encode_cs_kernel(
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     half8* cimg = reinterpret_cast<half8*>(smem);
     unsigned char* stg_all = smem + FR * 16;
-    float* hb = reinterpret_cast<float*>(stg_all + kWaves * 32 * PITCH);
+    constexpr int NT = NW * 64;
+    constexpr int kDep = NW == kWaves ? kDepth : 2;  // x blocks in flight per wave
+    float* hb = reinterpret_cast<float*>(stg_all + NW * 32 * PITCH);
     float* cnl = hb + 256;
     int* ctr = reinterpret_cast<int*>(cnl + 256);  // [0] pairs, [1] full, [2] resolve batches
-    constexpr int kProd = kWaves;  // streaming waves
+    constexpr int kProd = NW;  // streaming waves
 
     const int dsub = DS > 0 ? DS : dsub_in;
     const int tid = threadIdx.x;
@@ -227,9 +232,9 @@ __global__ __launch_bounds__(kThreads) void pq_encode_cs_kernel(
 
     {  // stage the subspace's fp16 codebook image, norms; zero the tiles (pad columns stay 0)
         const half8* src = img + (int64_t)m * FR;
-        for (int f = tid; f < FR; f += kThreads) cimg[f] = src[f];
+        for (int f = tid; f < FR; f += NT) cimg[f] = src[f];
         uint4* z = reinterpret_cast<uint4*>(stg_all);
-        for (int f = tid; f < kWaves * 32 * PITCH / 16; f += kThreads) z[f] = make_uint4(0u, 0u, 0u, 0u);
+        for (int f = tid; f < NW * 32 * PITCH / 16; f += NT) z[f] = make_uint4(0u, 0u, 0u, 0u);
         if (tid < 256) {
             hb[tid] = hinit[(int64_t)m * 256 + tid];
             cnl[tid] = cn[(int64_t)m * 256 + tid];
@@ -340,8 +345,8 @@ __global__ __launch_bounds__(kThreads) void pq_encode_cs_kernel(
         }
     };
 
-    // One step encodes block vb from registers xr and refills xr with block vb + kDepth*kWaves
-    // right after staging it, so kDepth blocks per wave are in flight.
+    // One step encodes block vb from registers xr and refills xr with block vb + kDep*NW
+    // right after staging it, so kDep blocks per wave are in flight.
     auto step = [&](const int vb, float4 (&xr)[NIMAX]) __attribute__((always_inline)) {
         // sigma * x -> fp16 -> this wave's tile (LAYOUT 0: lanes past the block's rows skip)
         // sigma == 1 (ordinary codebook magnitudes, pq_prep_mfma_kernel): no scaling multiply
@@ -373,7 +378,7 @@ __global__ __launch_bounds__(kThreads) void pq_encode_cs_kernel(
             xx = dot2_self(u[0], xx); xx = dot2_self(u[1], xx);
             xx = dot2_self(u[2], xx); xx = dot2_self(u[3], xx);
         }
-        if (vb + kDepth * kProd < nvb && !((V & 64) && vb >= kProd)) load(vb + kDepth * kProd, xr);
+        if (vb + kDep * kProd < nvb && !((V & 64) && vb >= kProd)) load(vb + kDep * kProd, xr);
         xx += __shfl_xor(xx, 32);
 
         // Candidates: the 16 packed scores of centroid block cb in this lane form a group; each
@@ -483,10 +488,10 @@ __global__ __launch_bounds__(kThreads) void pq_encode_cs_kernel(
         float4 xa[NIMAX], xb[NIMAX];
         int vb = w;
         if (vb < nvb) load(vb, xa);
-        if (kDepth == 2 && vb + kProd < nvb) load(vb + kProd, xb);
-        for (; vb < nvb; vb += kDepth * kProd) {
+        if (kDep == 2 && vb + kProd < nvb) load(vb + kProd, xb);
+        for (; vb < nvb; vb += kDep * kProd) {
             step(vb, xa);
-            if (kDepth == 1) continue;
+            if (kDep == 1) continue;
             if (vb + kProd >= nvb) break;
             step(vb + kProd, xb);
         }
@@ -1221,9 +1226,15 @@ constexpr int kMWaves = 4;
 template <int KS>
 __device__ __forceinline__ int cswz(int k) { return (4 * KS) % 8 == 0 ? (k & 7) : (k & 3); }
 
+// Wide subspaces (KS > 6): the fp32 codebook (up to 192 KiB) does not fit in LDS; the
+// canonical chains read the centroid rows from C itself (L2-resident) and the full batches
+// load the A operands one centroid block at a time.
+template <int KS>
+constexpr bool merged_gc() { return KS > 6; }
+
 template <int KS>
 constexpr int merged_smem_bytes() {
-    return 256 * 16 * KS * 4 + 2 * 256 * 4 + 16 + kMWaves * (32 * (16 * KS + 4) * 4);
+    return (merged_gc<KS>() ? 0 : 256 * 16 * KS * 4) + 2 * 256 * 4 + 16 + kMWaves * (32 * (16 * KS + 4) * 4);
 }
 
 // V (profiling, tools/cs_variants.hip): 1 << 21 skips the full batches, 1 << 22 the pair
@@ -1242,8 +1253,9 @@ __global__ __launch_bounds__(kMWaves * 64) __attribute__((amdgpu_waves_per_eu(1,
     const int dsub = DS > 0 ? DS : dsub_in;
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     constexpr int CP = DP;
-    float* cl = reinterpret_cast<float*>(smem);  // [256][DP], chunks swizzled (cswz)
-    float* cnl = cl + 256 * CP;
+    constexpr bool GC = merged_gc<KS>();
+    float* cl = reinterpret_cast<float*>(smem);  // [256][DP], chunks swizzled (cswz); GC: none
+    float* cnl = cl + (GC ? 0 : 256 * CP);
     float* hb = cnl + 256;
     int* ctr = reinterpret_cast<int*>(hb + 256);
     const int tid = threadIdx.x;
@@ -1264,7 +1276,7 @@ __global__ __launch_bounds__(kMWaves * 64) __attribute__((amdgpu_waves_per_eu(1,
     if (np + nf == 0) return;
     const float* Cm = C + (int64_t)m * 256 * dsub;
     {  // the fp32 codebook, zero-padded to DP; 16-B copies, 8 in flight per thread
-        const int q4 = DP >> 2, tot = 256 * q4;
+        const int q4 = DP >> 2, tot = GC ? 0 : 256 * q4;
         for (int e0 = tid; e0 < tot; e0 += 8 * kMWaves * 64) {
             f32x4 v[8];
 #pragma unroll
@@ -1320,10 +1332,11 @@ __global__ __launch_bounds__(kMWaves * 64) __attribute__((amdgpu_waves_per_eu(1,
 #pragma unroll
         for (int t = 0; t < NQ; ++t) xv[t] = *reinterpret_cast<const f32x4*>(xr + 4 * t);
     };
-    // canonical score of centroid k for the staged row xr (sequential fmaf chain over t), any dsub
+    // canonical score of centroid k for the staged row xr (sequential fmaf chain over t), any
+    // dsub; GC: the centroid row straight from C (unswizzled)
     auto exact = [&](const float* xr, int k) __attribute__((always_inline)) {
-        const float* c = cl + k * CP;
-        const int sw = cswz<KS>(k);
+        const float* c = GC ? Cm + (int64_t)k * dsub : cl + k * CP;
+        const int sw = GC ? 0 : cswz<KS>(k);
         float dot = 0.0f;
 #pragma unroll 2
         for (int t = 0; t < (DS > 0 ? DS : dsub); t += 4) {
@@ -1338,10 +1351,14 @@ __global__ __launch_bounds__(kMWaves * 64) __attribute__((amdgpu_waves_per_eu(1,
     };
     // 32 sub-rows (row offsets in rowl of lanes 0..cntb-1) into the wave's staging tile
     auto gather = [&](int cntb, int rowl) __attribute__((always_inline)) {
+        // the lane index through an opaque move: the per-j offsets are recomputed per gather
+        // (a few VALU) instead of being hoisted out of the batch loop (2 NL registers)
+        int lv;
+        asm volatile("v_mov_b32 %0, %1" : "=v"(lv) : "v"(l));
         f32x4 v[NL];
 #pragma unroll
         for (int j = 0; j < NL; ++j) {
-            const int c = j * 64 + l;
+            const int c = j * 64 + lv;
             const int row = c / q, col = c - row * q;
             const int src = __shfl(rowl, min(row, 31));
             const bool ok = j < nld && row < cntb;
@@ -1349,7 +1366,7 @@ __global__ __launch_bounds__(kMWaves * 64) __attribute__((amdgpu_waves_per_eu(1,
         }
 #pragma unroll
         for (int j = 0; j < NL; ++j) {
-            const int c = j * 64 + l;
+            const int c = j * 64 + lv;
             const int row = c / q, col = c - row * q;
             if (j < nld && row < 32) *reinterpret_cast<f32x4*>(xf + row * XP + 4 * col) = v[j];
         }
@@ -1385,12 +1402,15 @@ __global__ __launch_bounds__(kMWaves * 64) __attribute__((amdgpu_waves_per_eu(1,
             if (l < cntb) rowl = (int)list[nrows - 1 - (first + l)].x;
             gather(cntb, rowl);
             // the filter's A operands (the prepared f16 image of C_m, L2-resident), all 8
-            // centroid blocks, in flight while the B operand is built
-            half8 aa[8][KS];
+            // centroid blocks, in flight while the B operand is built (GC: one block at a time
+            // in the sweep below)
+            half8 aa[GC ? 1 : 8][KS];
+            if constexpr (!GC) {
 #pragma unroll
-            for (int cb = 0; cb < 8; ++cb)
+                for (int cb = 0; cb < 8; ++cb)
 #pragma unroll
-                for (int ks = 0; ks < KS; ++ks) aa[cb][ks] = im[(cb * KS + ks) * 64 + l];
+                    for (int ks = 0; ks < KS; ++ks) aa[cb][ks] = im[(cb * KS + ks) * 64 + l];
+            }
             half8 bf[KS];
             float xx = 0.0f;
 #pragma unroll
@@ -1416,11 +1436,22 @@ __global__ __launch_bounds__(kMWaves * 64) __attribute__((amdgpu_waves_per_eu(1,
                     acc[cb][4 * qq + 2] = hv.z; acc[cb][4 * qq + 3] = hv.w;
                 }
             }
+            if constexpr (GC) {
 #pragma unroll
-            for (int ks = 0; ks < KS; ++ks)
+                for (int cb = 0; cb < 8; ++cb) {
 #pragma unroll
-                for (int cb = 0; cb < 8; ++cb)
-                    acc[cb] = __builtin_amdgcn_mfma_f32_32x32x16_f16(aa[cb][ks], bf[ks], acc[cb], 0, 0, 0);
+                    for (int ks = 0; ks < KS; ++ks) aa[0][ks] = im[(cb * KS + ks) * 64 + l];
+#pragma unroll
+                    for (int ks = 0; ks < KS; ++ks)
+                        acc[cb] = __builtin_amdgcn_mfma_f32_32x32x16_f16(aa[0][ks], bf[ks], acc[cb], 0, 0, 0);
+                }
+            } else {
+#pragma unroll
+                for (int ks = 0; ks < KS; ++ks)
+#pragma unroll
+                    for (int cb = 0; cb < 8; ++cb)
+                        acc[cb] = __builtin_amdgcn_mfma_f32_32x32x16_f16(aa[cb][ks], bf[ks], acc[cb], 0, 0, 0);
+            }
             float t1 = -INFINITY;
 #pragma unroll
             for (int cb = 0; cb < 8; ++cb)
@@ -1569,12 +1600,12 @@ int device_cus() {
 }
 
 // Chunk count for one workgroup per CU at a time: minimise the rounds of workgroups per row
-// (ceil(chunks*M / CUs) / chunks), preferring fewer chunks, with at least 32*kWaves rows each
+// (ceil(chunks*M / CUs) / chunks), preferring fewer chunks, with at least 32 nw rows each
 // and few enough rows that a chunk's buffer offsets fit 31 bits.
-int64_t pick_chunks(int64_t n, int d, int M, int cus) {
+int64_t pick_chunks(int64_t n, int d, int M, int cus, int nw) {
     const int64_t rmax = std::max<int64_t>(32, ((int64_t)1 << 31) / ((int64_t)d * 4) - 64);
     const int64_t cmin = ceil_div(n, rmax);
-    const int64_t cmax = std::max<int64_t>(cmin, std::min<int64_t>(ceil_div(n, 32 * kWaves), 4 * (int64_t)cus));
+    const int64_t cmax = std::max<int64_t>(cmin, std::min<int64_t>(ceil_div(n, 32 * nw), 4 * (int64_t)cus));
     int64_t best = cmin;
     double best_cost = 1e300;
     for (int64_t c = cmin; c <= cmax; ++c) {
@@ -1588,7 +1619,7 @@ int64_t pick_chunks(int64_t n, int d, int M, int cus) {
 
 int cs_smem_bytes(int KS, int dsub) {
     (void)dsub;
-    return 8 * KS * 64 * 16 + kWaves * 32 * (32 * KS + 16) + 2 * 256 * 4 + 16;
+    return 8 * KS * 64 * 16 + cs_waves(KS) * 32 * (32 * KS + 16) + 2 * 256 * 4 + 16;
 }
 
 // Load layout for dsub (see the kernel): period-P flat layouts where all lanes stay busy.
@@ -1606,26 +1637,23 @@ hipError_t launch_pq_encode_cs_v(const float* x, int64_t n, int d, int M, int ds
                                  uint8_t* codesT, void* items, void* counts, void* pinfo, hipStream_t st) {
     const int smem = cs_smem_bytes(KS, dsub);
     const int layout = cs_layout(dsub);
-    auto kern = layout == 1 ? pq_encode_cs_kernel<KS, 1, V>
-              : layout == 3 ? pq_encode_cs_kernel<KS, 3, V> : pq_encode_cs_kernel<KS, 0, V>;
+    constexpr int NW = cs_waves(KS);
+    auto kern = layout == 1 ? pq_encode_cs_kernel<KS, 1, V, 0, NW>
+              : layout == 3 ? pq_encode_cs_kernel<KS, 3, V, 0, NW> : pq_encode_cs_kernel<KS, 0, V, 0, NW>;
     if constexpr (KS == 6) {
         if (dsub == 96) kern = pq_encode_cs_kernel<6, 3, V, 96>;
     }
     hipError_t e = hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, smem);
     if (e != hipSuccess) return e;
-    constexpr int rsmem = resolve_smem_bytes<KS>();
-    auto rkern = pq_resolve_cs_kernel<KS, V>;
-    e = hipFuncSetAttribute((const void*)rkern, hipFuncAttributeMaxDynamicSharedMemorySize, rsmem);
-    if (e != hipSuccess) return e;
     const int cus = device_cus();
-    const int64_t chunks = pick_chunks(n, d, M, cus);
+    const int64_t chunks = pick_chunks(n, d, M, cus, NW);
     const int64_t R = align_up(ceil_div(n, chunks), (int64_t)32);
     const int64_t grid = ceil_div(n, R) * M;
     // V & (1 << 20): the round-1 resolve (pair window in the pair kernel, separate full-item
     // and pair kernels), kept for A/B profiling
     constexpr bool legacy = (V & (1 << 20)) != 0;
     const float2* pdw = legacy ? nullptr : static_cast<const float2*>(pd);
-    hipLaunchKernelGGL(kern, dim3((unsigned)grid), dim3(kThreads), smem, st, x, n, d, M, dsub, R, C, cn,
+    hipLaunchKernelGGL(kern, dim3((unsigned)grid), dim3(NW * 64), smem, st, x, n, d, M, dsub, R, C, cn,
                        static_cast<const half8*>(img), hinit, static_cast<const float4*>(bnd), codesT,
                        static_cast<uint2*>(items), static_cast<int2*>(counts), static_cast<float2*>(pinfo), pdw,
                        static_cast<const float4*>(bnd2));
@@ -1642,7 +1670,11 @@ hipError_t launch_pq_encode_cs_v(const float* x, int64_t n, int d, int M, int ds
                            static_cast<const half8*>(img), hinit, static_cast<const float4*>(bnd), codesT,
                            static_cast<const uint2*>(items), static_cast<const int2*>(counts));
         return hipGetLastError();
-    }
+    } else {
+    constexpr int rsmem = resolve_smem_bytes<KS>();
+    auto rkern = pq_resolve_cs_kernel<KS, V>;
+    e = hipFuncSetAttribute((const void*)rkern, hipFuncAttributeMaxDynamicSharedMemorySize, rsmem);
+    if (e != hipSuccess) return e;
     // full items through pq_resolve_full_kernel (filter re-run + candidate chains): 1.5-2 %
     // faster end to end than the pair kernel's 256-wide scans (interleaved A/B, 1M x 1536);
     // V&256 restores the scans
@@ -1675,9 +1707,11 @@ hipError_t launch_pq_encode_cs_v(const float* x, int64_t n, int d, int M, int ds
                        (V & 32768) ? nullptr : static_cast<const float2*>(pd), static_cast<const float4*>(bnd2),
                        static_cast<const float2*>(pinfo));
     return hipGetLastError();
+    }
 }
 
-size_t cs_counts_bytes(int64_t n, int M) { return (size_t)ceil_div(n, 32 * kWaves) * M * sizeof(int2); }
+// (at most ceil(n / (32 nw)) row chunks per subspace; nw >= kWideWaves)
+size_t cs_counts_bytes(int64_t n, int M) { return (size_t)ceil_div(n, 32 * kWideWaves) * M * sizeof(int2); }
 
 hipError_t launch_pq_encode_cs(int KS, const float* x, int64_t n, int d, int M, int dsub, const float* C,
                                const float* cn, const void* img, const float* hinit, const void* bnd, const void* pd,
@@ -1691,6 +1725,7 @@ hipError_t launch_pq_encode_cs(int KS, const float* x, int64_t n, int d, int M, 
                                         pinfo, st);                                                            \
         break;
         MIVQ_CS_CASE(1) MIVQ_CS_CASE(2) MIVQ_CS_CASE(3) MIVQ_CS_CASE(4) MIVQ_CS_CASE(5) MIVQ_CS_CASE(6)
+        MIVQ_CS_CASE(7) MIVQ_CS_CASE(8) MIVQ_CS_CASE(9) MIVQ_CS_CASE(10) MIVQ_CS_CASE(11) MIVQ_CS_CASE(12)
 #undef MIVQ_CS_CASE
         default: return hipErrorInvalidValue;
     }

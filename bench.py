@@ -353,7 +353,7 @@ def opq32_leg(a, dev, steps, warmup):
             "value": n / wall, "unit": "vectors/s", "ms_per_step": wall * 1e3, "dtype": "f32",
             "config": {"workload": f"opq32_encode_{n}x{d}", "M": M, "nbits": 8, "opq_outer_iters": a.opq_iters,
                        "fit_s": t_fit, "data": a.data},
-            "roofline": {"bound": "mfma", "kernel": _native.opq_backend() if split else "opq_gemm_kernel (fp32 MFMA)",
+            "roofline": {"bound": "mfma", "kernel": _native.opq_backend(d) if split else "opq_gemm_kernel (fp32 MFMA)",
                          "achieved": tfs, "peak": peak, "unit": "TFLOP/s (fp32-accurate)", "frac": tfs / peak,
                          "peak_note": "dense f16 MFMA peak / 3 (x_hi b_hi + x_hi b_lo + x_lo b_hi)" if split else
                                       "dense fp32 MFMA peak", "vs_fp32_mfma_peak": tfs / MFMA_F32_PEAK_TFS,

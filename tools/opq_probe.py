@@ -1,5 +1,5 @@
 """Run the prepared OPQ rotation (1M x 1536 by default) a few times: a short program for
-rocprofv3 --pmc / --kernel-trace passes over opq_split_gemm_kernel.
+rocprofv3 --pmc / --kernel-trace passes over the split-f16 rotation kernels.
 
 usage: python tools/opq_probe.py [--n 1000000] [--d 1536] [--reps 5]
 """
@@ -19,6 +19,8 @@ def main():
     ap.add_argument("--n", type=int, default=1_000_000)
     ap.add_argument("--d", type=int, default=1536)
     ap.add_argument("--reps", type=int, default=5)
+    ap.add_argument("--lib-gemm", action="store_true",
+                    help="also time one plain f16 / bf16 library GEMM (torch.matmul) of the same shape")
     a = ap.parse_args()
     dev = _native.require_device()
     g = torch.Generator(device=dev).manual_seed(0)
@@ -38,6 +40,20 @@ def main():
     torch.cuda.synchronize()
     ms = s.elapsed_time(e) / a.reps
     print(f"opq rotate {a.n}x{a.d}: {ms:.3f} ms/call = {2 * a.n * a.d * a.d / (ms * 1e-3) / 1e12:.1f} TF/s", flush=True)
+    if a.lib_gemm:  # a yardstick: what one library f16 GEMM of this shape costs
+        for dt in (torch.float16, torch.bfloat16):
+            xh, bh = x.to(dt), A.to(dt)
+            for _ in range(2):
+                torch.matmul(xh, bh)
+            torch.cuda.synchronize()
+            s.record()
+            for _ in range(a.reps):
+                torch.matmul(xh, bh)
+            e.record()
+            torch.cuda.synchronize()
+            ms = s.elapsed_time(e) / a.reps
+            print(f"library {dt} GEMM {a.n}x{a.d}x{a.d}: {ms:.3f} ms = "
+                  f"{2 * a.n * a.d * a.d / (ms * 1e-3) / 1e12:.1f} TF/s", flush=True)
 
 
 if __name__ == "__main__":

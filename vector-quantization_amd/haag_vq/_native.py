@@ -272,9 +272,11 @@ def opq_rotate(x: torch.Tensor, A: torch.Tensor, transpose: bool = False,
     return out
 
 
-def opq_backend() -> str:
-    """What the OPQ classes rotate with (for reports)."""
-    return "opq_split_gemm_kernel: split-f16 MFMA GEMM, fp32 accuracy"
+def opq_backend(d: Optional[int] = None) -> str:
+    """What the OPQ classes rotate with (for reports); d selects the kernel as opq.hip does."""
+    if d is not None and d % 32 == 0 and d >= 256:
+        return "opq_split_x_kernel + opq_glds_gemm_kernel: split-f16 MFMA GEMM (LDS-DMA staging), fp32 accuracy"
+    return "opq_row_scale_kernel + opq_split_gemm_kernel: split-f16 MFMA GEMM, fp32 accuracy"
 
 
 def opq_prepare(A: torch.Tensor, transpose: bool = False) -> Optional[torch.Tensor]:

@@ -1295,7 +1295,10 @@ __global__ __launch_bounds__(kMWaves * 64) __attribute__((amdgpu_waves_per_eu(1,
         }
         cnl[tid] = cn[(int64_t)m * 256 + tid];
         hb[tid] = hinit[(int64_t)m * 256 + tid];
-        if (tid == 0) ctr[0] = 0;
+        if (tid == 0) {
+            ctr[0] = 0;
+            ctr[1] = kMWaves;  // pair batches 0..kMWaves-1 are the waves' first (static)
+        }
     }
     __syncthreads();
     const half8* im = img + (int64_t)m * FR;
@@ -1315,16 +1318,25 @@ __global__ __launch_bounds__(kMWaves * 64) __attribute__((amdgpu_waves_per_eu(1,
     auto exact_reg = [&](const f32x4 (&xv)[NQ], int k) __attribute__((always_inline)) {
         const float* c = cl + k * CP;
         const int sw = cswz<KS>(k);
-        f32x4 cv[NQ];
-#pragma unroll
-        for (int t = 0; t < NQ; ++t) cv[t] = *reinterpret_cast<const f32x4*>(c + 4 * (t ^ sw));
+        // the centroid row in two halves (register budget: the pair loop holds a prefetched
+        // gather next to the row)
+        constexpr int NH = (NQ + 1) / 2;
         float dot = 0.0f;
 #pragma unroll
-        for (int t = 0; t < NQ; ++t) {
-            dot = __builtin_fmaf(xv[t].x, cv[t].x, dot);
-            dot = __builtin_fmaf(xv[t].y, cv[t].y, dot);
-            dot = __builtin_fmaf(xv[t].z, cv[t].z, dot);
-            dot = __builtin_fmaf(xv[t].w, cv[t].w, dot);
+        for (int t0 = 0; t0 < NQ; t0 += NH) {
+            f32x4 cv[NH];
+#pragma unroll
+            for (int t = 0; t < NH; ++t)
+                if (t0 + t < NQ) cv[t] = *reinterpret_cast<const f32x4*>(c + 4 * ((t0 + t) ^ sw));
+#pragma unroll
+            for (int t = 0; t < NH; ++t) {
+                if (t0 + t < NQ) {
+                    dot = __builtin_fmaf(xv[t0 + t].x, cv[t].x, dot);
+                    dot = __builtin_fmaf(xv[t0 + t].y, cv[t].y, dot);
+                    dot = __builtin_fmaf(xv[t0 + t].z, cv[t].z, dot);
+                    dot = __builtin_fmaf(xv[t0 + t].w, cv[t].w, dot);
+                }
+            }
         }
         return __builtin_fmaf(-2.0f, dot, cnl[k]);
     };
@@ -1349,13 +1361,16 @@ __global__ __launch_bounds__(kMWaves * 64) __attribute__((amdgpu_waves_per_eu(1,
         }
         return __builtin_fmaf(-2.0f, dot, cnl[k]);
     };
-    // 32 sub-rows (row offsets in rowl of lanes 0..cntb-1) into the wave's staging tile
-    auto gather = [&](int cntb, int rowl) __attribute__((always_inline)) {
+    // The rows of a batch (row offsets in rowl of lanes 0..cntb-1) are gathered in two halves:
+    // gather_issue puts the 16-B loads in flight into registers, gather_commit writes them to
+    // the wave's staging tile.  The loop issues batch b+1's gather before it computes batch b
+    // (after a full batch's A-operand loads, so waiting for those never waits for the prefetch):
+    // each wave keeps one batch of row gathers in flight while it computes.
+    auto gather_issue = [&](int cntb, int rowl, f32x4 (&v)[NL]) __attribute__((always_inline)) {
         // the lane index through an opaque move: the per-j offsets are recomputed per gather
         // (a few VALU) instead of being hoisted out of the batch loop (2 NL registers)
         int lv;
         asm volatile("v_mov_b32 %0, %1" : "=v"(lv) : "v"(l));
-        f32x4 v[NL];
 #pragma unroll
         for (int j = 0; j < NL; ++j) {
             const int c = j * 64 + lv;
@@ -1364,6 +1379,10 @@ __global__ __launch_bounds__(kMWaves * 64) __attribute__((amdgpu_waves_per_eu(1,
             const bool ok = j < nld && row < cntb;
             v[j] = *reinterpret_cast<const f32x4*>(xsub + (ok ? (int64_t)src * d + 4 * col : 0));
         }
+    };
+    auto gather_commit = [&](const f32x4 (&v)[NL]) __attribute__((always_inline)) {
+        int lv;
+        asm volatile("v_mov_b32 %0, %1" : "=v"(lv) : "v"(l));
 #pragma unroll
         for (int j = 0; j < NL; ++j) {
             const int c = j * 64 + lv;
@@ -1377,33 +1396,155 @@ __global__ __launch_bounds__(kMWaves * 64) __attribute__((amdgpu_waves_per_eu(1,
             }
         lds_fence();
     };
+    // batch b's items: lanes with r < cntb hold (row, k1 | k2 << 8) (full items: (row, 0))
+    auto batch_info = [&](int b, uint2& it, int& cntb) __attribute__((always_inline)) {
+        const bool full = b < nbf;
+        const int first = (full ? b : b - nbf) * 32;
+        cntb = min(32, (full ? nf : np) - first);
+        // unconditional (clamped) load: no load sits on a divergent path, so the compiler's
+        // wait-count bookkeeping stays exact around the prefetched gathers
+        const int e = full ? nrows - 1 - (first + r) : first + r;
+        const uint2 v = list[r < cntb ? e : 0];
+        it = r < cntb ? v : make_uint2(0u, 0u);
+    };
 
-    for (;;) {
-        int b = 0;
-        if (l == 0) b = atomicAdd(&ctr[0], 1);
-        b = __shfl(b, 0);
-        if (b >= nbf + nbp) break;
+    // full batch (rows staged): one MFMA sweep with the A operands aa, window mask, chains
+    auto full_batch = [&](const half8 (&aa)[GC ? 1 : 8][KS], int cntb, int rowl) __attribute__((always_inline)) {
         const float* xr = xf + r * XP;
-        if constexpr ((V & (3 << 21)) != 0) {
-            if (((V & (1 << 21)) && b < nbf) || ((V & (1 << 22)) && b >= nbf)) continue;
+        half8 bf[KS];
+        float xx = 0.0f;
+#pragma unroll
+        for (int ks = 0; ks < KS; ++ks) {
+            const float* src = xr + h * 8 * KS + 8 * ks;
+            const f32x4 a0 = *reinterpret_cast<const f32x4*>(src);
+            const f32x4 a1 = *reinterpret_cast<const f32x4*>(src + 4);
+            const float2v p0 = (float2v){a0.x, a0.y} * sig2, p1 = (float2v){a0.z, a0.w} * sig2;
+            const float2v p2 = (float2v){a1.x, a1.y} * sig2, p3 = (float2v){a1.z, a1.w} * sig2;
+            const u32x4 u = (u32x4){cvt2(p0.x, p0.y), cvt2(p1.x, p1.y), cvt2(p2.x, p2.y), cvt2(p3.x, p3.y)};
+            bf[ks] = __builtin_bit_cast(half8, u);
+            xx = dot2_self(u[0], xx); xx = dot2_self(u[1], xx);
+            xx = dot2_self(u[2], xx); xx = dot2_self(u[3], xx);
         }
-        if constexpr ((V & (1 << 23)) != 0) {
-            const int first = (b < nbf ? b : b - nbf) * 32;
-            const int cntb = min(32, (b < nbf ? nf : np) - first);
-            int rowl = 0;
-            if (l < cntb) rowl = (int)(b < nbf ? list[nrows - 1 - (first + l)].x : list[first + l].x);
-            gather(cntb, rowl);
-            continue;
+        xx += __shfl_xor(xx, 32);
+        floatx16 acc[8];
+#pragma unroll
+        for (int cb = 0; cb < 8; ++cb) {
+#pragma unroll
+            for (int qq = 0; qq < 4; ++qq) {
+                const float4 hv = *reinterpret_cast<const float4*>(hb + cb * 32 + 8 * qq + 4 * h);
+                acc[cb][4 * qq + 0] = hv.x; acc[cb][4 * qq + 1] = hv.y;
+                acc[cb][4 * qq + 2] = hv.z; acc[cb][4 * qq + 3] = hv.w;
+            }
         }
-        if (b < nbf) {
-            const int first = b * 32;
-            const int cntb = min(32, nf - first);
-            int rowl = 0;
-            if (l < cntb) rowl = (int)list[nrows - 1 - (first + l)].x;
-            gather(cntb, rowl);
-            // the filter's A operands (the prepared f16 image of C_m, L2-resident), all 8
-            // centroid blocks, in flight while the B operand is built (GC: one block at a time
-            // in the sweep below)
+        if constexpr (GC) {
+#pragma unroll
+            for (int cb = 0; cb < 8; ++cb) {
+                half8 a1[KS];
+#pragma unroll
+                for (int ks = 0; ks < KS; ++ks) a1[ks] = im[(cb * KS + ks) * 64 + l];
+#pragma unroll
+                for (int ks = 0; ks < KS; ++ks)
+                    acc[cb] = __builtin_amdgcn_mfma_f32_32x32x16_f16(a1[ks], bf[ks], acc[cb], 0, 0, 0);
+            }
+        } else {
+#pragma unroll
+            for (int ks = 0; ks < KS; ++ks)
+#pragma unroll
+                for (int cb = 0; cb < 8; ++cb)
+                    acc[cb] = __builtin_amdgcn_mfma_f32_32x32x16_f16(aa[cb][ks], bf[ks], acc[cb], 0, 0, 0);
+        }
+        float t1 = -INFINITY;
+#pragma unroll
+        for (int cb = 0; cb < 8; ++cb)
+#pragma unroll
+            for (int i = 0; i < 16; ++i) t1 = fmaxf(t1, acc[cb][i]);
+        t1 = fmaxf(t1, __shfl_xor(t1, 32));
+        const float Xs = (__builtin_amdgcn_sqrtf(xx) * (1.0f + 1e-5f) + xs_eta) * (1.0f + 9.765625e-4f);
+        const float W = bm.y * Xs + bm.z;
+        const float thr = t1 - W;
+        const bool bad = !(Xs < 65000.0f) || !isfinite(t1) || !isfinite(W);
+        if constexpr ((V & (1 << 25)) != 0) {
+            if (h == 0 && r < cntb) codesT[(int64_t)m * n + r0 + rowl] = (uint8_t)(__float_as_uint(thr) & 0xFF);
+            return;
+        }
+        // this lane's centroids inside the window as a 128-bit mask (4 words of two centroid
+        // blocks; register-only, no per-value LDS stores), then their canonical chains in
+        // increasing k, one loop for all of them; a row the window cannot vouch for takes
+        // all 128 of the lane's centroids
+        uint32_t wm[4];
+#pragma unroll
+        for (int q2 = 0; q2 < 4; ++q2) {
+            uint32_t mm = 0u;
+#pragma unroll
+            for (int i = 0; i < 32; ++i) mm |= acc[2 * q2 + (i >> 4)][i & 15] >= thr ? (1u << i) : 0u;
+            wm[q2] = bad ? 0xFFFFFFFFu : mm;
+        }
+        float bs = INFINITY;
+        int bk = 256;
+        auto take = [&](float sc, int k) __attribute__((always_inline)) {
+            if (sc < bs || (sc == bs && k < bk)) { bs = sc; bk = k; }
+        };
+        if (r < cntb && !(V & (1 << 24))) {
+            f32x4 xv[NQ];
+            if constexpr (DS > 0) load_row(xr, xv);
+            while ((wm[0] | wm[1] | wm[2] | wm[3]) != 0u) {
+                const int wi = wm[0] ? 0 : wm[1] ? 1 : wm[2] ? 2 : 3;
+                const uint32_t wsel = wm[0] ? wm[0] : wm[1] ? wm[1] : wm[2] ? wm[2] : wm[3];
+                const int bit = __builtin_ctz(wsel);
+                const uint32_t rest = wsel & (wsel - 1u);
+                wm[0] = wi == 0 ? rest : wm[0];
+                wm[1] = wi == 1 ? rest : wm[1];
+                wm[2] = wi == 2 ? rest : wm[2];
+                wm[3] = wi == 3 ? rest : wm[3];
+                const int cb = 2 * wi + (bit >> 4), i = bit & 15;
+                const int k = cb * 32 + (i & 3) + 8 * (i >> 2) + 4 * h;
+                if constexpr (DS > 0) take(exact_reg(xv, k), k);
+                else take(exact(xr, k), k);
+            }
+        }
+        const float os = __shfl_xor(bs, 32);
+        const int ok = __shfl_xor(bk, 32);
+        if (os < bs || (os == bs && ok < bk)) { bs = os; bk = ok; }
+        if (h == 0 && r < cntb) codesT[(int64_t)m * n + r0 + rowl] = (uint8_t)((bs < INFINITY) ? bk : 0);
+    };
+    // pair batch (rows staged): lane (r, 0) runs the chain of k1, lane (r, 1) that of k2
+    auto pair_batch = [&](int cntb, uint2 it) __attribute__((always_inline)) {
+        const float* xr = xf + r * XP;
+        const int rowl = (int)it.x;
+        const int k1 = (int)(it.y & 0xFFu), k2 = (int)((it.y >> 8) & 0xFFu);
+        const int kk = h ? k2 : k1;
+        float sc = 0.0f;
+        if (r < cntb) {
+            if constexpr (DS > 0) {
+                f32x4 xv[NQ];
+                load_row(xr, xv);
+                sc = exact_reg(xv, kk);
+            } else {
+                sc = exact(xr, kk);
+            }
+        }
+        const float os = __shfl_xor(sc, 32);
+        if (h == 0 && r < cntb) {
+            // (s1, k1) here, (s2, k2) from the partner: smallest (s, k), NaN never wins
+            const bool two = os < sc || (os == sc && k2 < k1) || (sc != sc && os == os);
+            codesT[(int64_t)m * n + r0 + rowl] = (uint8_t)(two ? k2 : k1);
+        }
+    };
+
+    // Full batches first (claimed from ctr[0]; their A operands take 192 registers, so their
+    // gathers are not prefetched), then pair batches (claimed from ctr[1]) with the next pair
+    // batch's gather in flight while the current one is computed.
+    if (!(V & (1 << 21)))
+        for (;;) {
+            int b = 0;
+            if (l == 0) b = atomicAdd(&ctr[0], 1);
+            b = __builtin_amdgcn_readfirstlane(__shfl(b, 0));
+            if (b >= nbf) break;
+            uint2 it;
+            int cntb;
+            batch_info(b, it, cntb);
+            f32x4 v[NL];
+            gather_issue(cntb, (int)it.x, v);
             half8 aa[GC ? 1 : 8][KS];
             if constexpr (!GC) {
 #pragma unroll
@@ -1411,130 +1552,39 @@ __global__ __launch_bounds__(kMWaves * 64) __attribute__((amdgpu_waves_per_eu(1,
 #pragma unroll
                     for (int ks = 0; ks < KS; ++ks) aa[cb][ks] = im[(cb * KS + ks) * 64 + l];
             }
-            half8 bf[KS];
-            float xx = 0.0f;
-#pragma unroll
-            for (int ks = 0; ks < KS; ++ks) {
-                const float* src = xr + h * 8 * KS + 8 * ks;
-                const f32x4 a0 = *reinterpret_cast<const f32x4*>(src);
-                const f32x4 a1 = *reinterpret_cast<const f32x4*>(src + 4);
-                const float2v p0 = (float2v){a0.x, a0.y} * sig2, p1 = (float2v){a0.z, a0.w} * sig2;
-                const float2v p2 = (float2v){a1.x, a1.y} * sig2, p3 = (float2v){a1.z, a1.w} * sig2;
-                const u32x4 u = (u32x4){cvt2(p0.x, p0.y), cvt2(p1.x, p1.y), cvt2(p2.x, p2.y), cvt2(p3.x, p3.y)};
-                bf[ks] = __builtin_bit_cast(half8, u);
-                xx = dot2_self(u[0], xx); xx = dot2_self(u[1], xx);
-                xx = dot2_self(u[2], xx); xx = dot2_self(u[3], xx);
-            }
-            xx += __shfl_xor(xx, 32);
-            floatx16 acc[8];
-#pragma unroll
-            for (int cb = 0; cb < 8; ++cb) {
-#pragma unroll
-                for (int qq = 0; qq < 4; ++qq) {
-                    const float4 hv = *reinterpret_cast<const float4*>(hb + cb * 32 + 8 * qq + 4 * h);
-                    acc[cb][4 * qq + 0] = hv.x; acc[cb][4 * qq + 1] = hv.y;
-                    acc[cb][4 * qq + 2] = hv.z; acc[cb][4 * qq + 3] = hv.w;
-                }
-            }
-            if constexpr (GC) {
-#pragma unroll
-                for (int cb = 0; cb < 8; ++cb) {
-#pragma unroll
-                    for (int ks = 0; ks < KS; ++ks) aa[0][ks] = im[(cb * KS + ks) * 64 + l];
-#pragma unroll
-                    for (int ks = 0; ks < KS; ++ks)
-                        acc[cb] = __builtin_amdgcn_mfma_f32_32x32x16_f16(aa[0][ks], bf[ks], acc[cb], 0, 0, 0);
-                }
-            } else {
-#pragma unroll
-                for (int ks = 0; ks < KS; ++ks)
-#pragma unroll
-                    for (int cb = 0; cb < 8; ++cb)
-                        acc[cb] = __builtin_amdgcn_mfma_f32_32x32x16_f16(aa[cb][ks], bf[ks], acc[cb], 0, 0, 0);
-            }
-            float t1 = -INFINITY;
-#pragma unroll
-            for (int cb = 0; cb < 8; ++cb)
-#pragma unroll
-                for (int i = 0; i < 16; ++i) t1 = fmaxf(t1, acc[cb][i]);
-            t1 = fmaxf(t1, __shfl_xor(t1, 32));
-            const float Xs = (__builtin_amdgcn_sqrtf(xx) * (1.0f + 1e-5f) + xs_eta) * (1.0f + 9.765625e-4f);
-            const float W = bm.y * Xs + bm.z;
-            const float thr = t1 - W;
-            const bool bad = !(Xs < 65000.0f) || !isfinite(t1) || !isfinite(W);
-            if constexpr ((V & (1 << 25)) != 0) {
-                if (h == 0 && r < cntb) codesT[(int64_t)m * n + r0 + rowl] = (uint8_t)(__float_as_uint(thr) & 0xFF);
-                lds_fence();
-                continue;
-            }
-            // this lane's centroids inside the window as a 128-bit mask (4 words of two centroid
-            // blocks; register-only, no per-value LDS stores), then their canonical chains in
-            // increasing k, one loop for all of them; a row the window cannot vouch for takes
-            // all 128 of the lane's centroids
-            uint32_t wm[4];
-#pragma unroll
-            for (int q2 = 0; q2 < 4; ++q2) {
-                uint32_t mm = 0u;
-#pragma unroll
-                for (int i = 0; i < 32; ++i) mm |= acc[2 * q2 + (i >> 4)][i & 15] >= thr ? (1u << i) : 0u;
-                wm[q2] = bad ? 0xFFFFFFFFu : mm;
-            }
-            float bs = INFINITY;
-            int bk = 256;
-            auto take = [&](float sc, int k) __attribute__((always_inline)) {
-                if (sc < bs || (sc == bs && k < bk)) { bs = sc; bk = k; }
-            };
-            if (r < cntb && !(V & (1 << 24))) {
-                f32x4 xv[NQ];
-                if constexpr (DS > 0) load_row(xr, xv);
-                while ((wm[0] | wm[1] | wm[2] | wm[3]) != 0u) {
-                    const int wi = wm[0] ? 0 : wm[1] ? 1 : wm[2] ? 2 : 3;
-                    const uint32_t wsel = wm[0] ? wm[0] : wm[1] ? wm[1] : wm[2] ? wm[2] : wm[3];
-                    const int bit = __builtin_ctz(wsel);
-                    const uint32_t rest = wsel & (wsel - 1u);
-                    wm[0] = wi == 0 ? rest : wm[0];
-                    wm[1] = wi == 1 ? rest : wm[1];
-                    wm[2] = wi == 2 ? rest : wm[2];
-                    wm[3] = wi == 3 ? rest : wm[3];
-                    const int cb = 2 * wi + (bit >> 4), i = bit & 15;
-                    const int k = cb * 32 + (i & 3) + 8 * (i >> 2) + 4 * h;
-                    if constexpr (DS > 0) take(exact_reg(xv, k), k);
-                    else take(exact(xr, k), k);
-                }
-            }
-            const float os = __shfl_xor(bs, 32);
-            const int ok = __shfl_xor(bk, 32);
-            if (os < bs || (os == bs && ok < bk)) { bs = os; bk = ok; }
-            if (h == 0 && r < cntb) codesT[(int64_t)m * n + r0 + rowl] = (uint8_t)((bs < INFINITY) ? bk : 0);
-            lds_fence();
-        } else {
-            // 32 pairs: lane (r, 0) runs the chain of k1, lane (r, 1) that of k2
-            const int first = (b - nbf) * 32;
-            const int cntb = min(32, np - first);
-            uint2 it = make_uint2(0u, 0u);
-            if (r < cntb) it = list[first + r];
-            const int rowl = (int)it.x;
-            gather(cntb, rowl);
-            const int k1 = (int)(it.y & 0xFFu), k2 = (int)((it.y >> 8) & 0xFFu);
-            const int kk = h ? k2 : k1;
-            float sc = 0.0f;
-            if (r < cntb) {
-                if constexpr (DS > 0) {
-                    f32x4 xv[NQ];
-                    load_row(xr, xv);
-                    sc = exact_reg(xv, kk);
-                } else {
-                    sc = exact(xr, kk);
-                }
-            }
-            const float os = __shfl_xor(sc, 32);
-            if (h == 0 && r < cntb) {
-                // (s1, k1) here, (s2, k2) from the partner: smallest (s, k), NaN never wins
-                const bool two = os < sc || (os == sc && k2 < k1) || (sc != sc && os == os);
-                codesT[(int64_t)m * n + r0 + rowl] = (uint8_t)(two ? k2 : k1);
-            }
-            lds_fence();
+            gather_commit(v);
+            if (!(V & (1 << 23))) full_batch(aa, cntb, (int)it.x);
+            lds_fence();  // the tile is rewritten by the next commit
         }
+    if (V & (1 << 22)) return;
+    // pair batches: the first one per wave is static (b = w), the rest are claimed from ctr[1]
+    int b = w, cntb = 0;
+    uint2 it = make_uint2(0u, 0u);
+    f32x4 va[NL], vb2[NL];
+    batch_info(nbf + b, it, cntb);
+    gather_issue(cntb, (int)it.x, va);
+    // one batch: stage vc (batch b), claim the next and put its gather into vn, compute b
+    auto iter = [&](const f32x4 (&vc)[NL], f32x4 (&vn)[NL]) __attribute__((always_inline)) {
+        int bn = 0;
+        if (l == 0) bn = atomicAdd(&ctr[1], 1);
+        bn = __builtin_amdgcn_readfirstlane(__shfl(bn, 0));
+        uint2 itn;
+        int cntn;
+        batch_info(nbf + bn, itn, cntn);  // past the end: cntn <= 0, no rows
+        // vc's gather and the list entries of bn: everything in flight is needed now
+        __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
+        gather_commit(vc);
+        gather_issue(cntn, (int)itn.x, vn);  // cntn <= 0: every lane reads row 0 (discarded)
+        if (!(V & (1 << 23))) pair_batch(cntb, it);
+        lds_fence();  // the tile is rewritten by the next commit
+        b = bn;
+        it = itn;
+        cntb = cntn;
+    };
+    while (b < nbp) {
+        iter(va, vb2);
+        if (b >= nbp) break;
+        iter(vb2, va);
     }
 }
 
@@ -1612,6 +1662,12 @@ int64_t pick_chunks(int64_t n, int d, int M, int cus, int nw) {
         const double cost = (double)ceil_div(c * M, (int64_t)cus) / (double)c;
         if (cost < best_cost * (1.0 - 1e-9)) { best_cost = cost; best = c; }
     }
+#ifdef MIVQ_CS_CHUNK_MULT
+    best = std::min<int64_t>(best * MIVQ_CS_CHUNK_MULT, std::max<int64_t>(best, ceil_div(n, 32 * nw)));
+#endif
+#ifdef MIVQ_CS_FORCE_CHUNKS
+    best = std::max<int64_t>(cmin, MIVQ_CS_FORCE_CHUNKS);
+#endif
     return best;
 }
 

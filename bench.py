@@ -165,9 +165,9 @@ def timed(fn, steps, warmup, world=1, dev=None, settle_ms=0.0):
     max over ranks, device ms/call mean).
 
     settle_ms > 0: after the W warmup calls, further untimed calls until the warm-up has kept
-    the GPU busy for settle_ms.  The MI355X's power management needs ~20 ms of continuous load
-    to settle: in a kernel trace of back-to-back 1M-row encodes the first call after idle runs
-    at 1.13 ms, calls 2-10 at 1.30-1.57 ms, and every call after ~20 ms at 1.16-1.29 ms
+    the GPU busy for settle_ms.  The MI355X's power management needs ~30 ms of continuous load
+    to settle: in kernel traces of back-to-back 1M-row encodes the filter launches average
+    1.35-1.37 ms over calls 1-10, 1.22 ms over calls 11-20 and 1.17-1.18 ms after that
     (profiles/r02_s10_power_transient.txt); timing K = 20 calls after W = 5 would average
     that transient into a steady-state throughput figure.  The count of extra calls is
     reported (SETTLE)."""

@@ -657,6 +657,11 @@ extern "C" int mivq_pq_prepare(const float* centroids, int32_t d, int32_t M, int
     unsigned char* p = static_cast<unsigned char*>(prep);
     hipStream_t st = as_stream(stream);
     const int64_t mk = (int64_t)M * L.ksub;
+    // pads between the regions are zeroed so that equal codebooks give byte-equal prep buffers
+    // (pd, the large table, is written in full by pq_prep_spread_kernel)
+    hipError_t me = hipMemsetAsync(p, 0, L.pd, st);
+    if (me == hipSuccess) me = hipMemsetAsync(p + L.bnd2, 0, L.total - L.bnd2, st);
+    if (me != hipSuccess) return set_error(MIVQ_ERR_HIP, "pq_prepare(memset): %s", hipGetErrorString(me));
     hipLaunchKernelGGL(pq_prep_norms_kernel, dim3((unsigned)ceil_div(mk, 256)), dim3(256), 0, st,
                        centroids, M, L.ksub, L.dsub, reinterpret_cast<float*>(p + L.cn),
                        reinterpret_cast<float*>(p + L.ct));
@@ -664,7 +669,6 @@ extern "C" int mivq_pq_prepare(const float* centroids, int32_t d, int32_t M, int
     if (rc) return rc;
     if (L.mfma) {
         uint32_t* spread = reinterpret_cast<uint32_t*>(p + L.spread);
-        if (hipMemsetAsync(spread, 0, sizeof(uint32_t) * 2 * (size_t)M, st) != hipSuccess) return check_launch("pq_prep_spread");
         float2* pd = M <= kPdMaxM ? reinterpret_cast<float2*>(p + L.pd) : nullptr;
         hipLaunchKernelGGL(pq_prep_spread_kernel, dim3(M, 16), dim3(256), 0, st, centroids, L.dsub, spread, pd);
         rc = check_launch("pq_prep_spread");

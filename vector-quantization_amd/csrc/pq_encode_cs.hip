@@ -229,6 +229,9 @@ __global__ __launch_bounds__(NW * 64) void pq_encode_cs_kernel(
     const int64_t r1 = min(n, r0 + rows_per_wg);
     if (r0 >= r1) return;
     const int nrows = (int)(r1 - r0);
+#ifdef MIVQ_CS_TIMESTAMPS  // probe (tools/dbg/wg_times.py): start / end of every workgroup
+    const uint64_t t_start = wall_clock64();
+#endif
 
     {  // stage the subspace's fp16 codebook image, norms; zero the tiles (pad columns stay 0)
         const half8* src = img + (int64_t)m * FR;
@@ -503,6 +506,12 @@ __global__ __launch_bounds__(NW * 64) void pq_encode_cs_kernel(
     }  // producers
     __syncthreads();
     if (tid == 0) counts[blockIdx.x] = make_int2(ctr[0], ctr[1]);
+#ifdef MIVQ_CS_TIMESTAMPS  // (into the pair-info region, unused on this path)
+    if (tid == 0) {
+        reinterpret_cast<unsigned long long*>(pinfo)[2 * blockIdx.x] = t_start;
+        reinterpret_cast<unsigned long long*>(pinfo)[2 * blockIdx.x + 1] = wall_clock64();
+    }
+#endif
 }
 
 // Resolve: settles the lists of one encode workgroup (same blockIdx -> (chunk, m) mapping).

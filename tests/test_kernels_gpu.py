@@ -96,6 +96,23 @@ def test_pq_encode_bit_exact_trained_codebooks(dev, oracle, kind):
     np.testing.assert_array_equal(_h(_native.pq_encode(Xd, C, prep, 8, flags_extra=_native.MIVQ_PQ_LEGACY_MFMA)), ref)
 
 
+def test_pq_encode_bit_exact_config5_shape(dev, oracle):
+    """D = 1024, M = 16 (dsub 64: the 16-wave filter specialisation of BASELINE config #5) on a
+    k-means codebook, 120k rows (many row chunks per subspace, a ragged last chunk)."""
+    from haag_vq import _native
+    from haag_vq.methods._kmeans import train_pq
+
+    rng = np.random.default_rng(5)
+    n, d, M = 120_003, 1024, 16
+    X = rng.standard_normal((n, d)).astype(np.float32)
+    X /= np.linalg.norm(X, axis=1, keepdims=True)
+    Xd = _t(X, dev)
+    C = train_pq(Xd[:20000], M, 8, niter=8)
+    ref = oracle.pq_encode(X, _h(C))
+    prep = _native.pq_prepare(C, 8)
+    np.testing.assert_array_equal(_h(_native.pq_encode(Xd, C, prep, 8)), ref)
+
+
 @pytest.mark.parametrize("nbits", [1, 2, 4, 8])
 def test_extrabitq_kernels_match_reference_fixture(dev, golden_dir, nbits):
     """Device encode/decode of the reference's ExtendedRaBitQuantizer model state."""

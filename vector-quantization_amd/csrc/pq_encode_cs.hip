@@ -212,7 +212,7 @@ __global__ __launch_bounds__(NW * 64) void pq_encode_cs_kernel(
     half8* cimg = reinterpret_cast<half8*>(smem);
     unsigned char* stg_all = smem + FR * 16;
     constexpr int NT = NW * 64;
-    constexpr int kDep = NW == kWaves ? kDepth : 2;  // x blocks in flight per wave
+    constexpr int kDep = NW >= kWaves ? kDepth : 2;  // x blocks in flight per wave
     float* hb = reinterpret_cast<float*>(stg_all + NW * 32 * PITCH);
     float* cnl = hb + 256;
     int* ctr = reinterpret_cast<int*>(cnl + 256);  // [0] pairs, [1] full, [2] resolve batches
@@ -1705,20 +1705,38 @@ hipError_t launch_pq_encode_cs_v(const float* x, int64_t n, int d, int M, int ds
     constexpr int NW = cs_waves(KS);
     auto kern = layout == 1 ? pq_encode_cs_kernel<KS, 1, V, 0, NW>
               : layout == 3 ? pq_encode_cs_kernel<KS, 3, V, 0, NW> : pq_encode_cs_kernel<KS, 0, V, 0, NW>;
+#ifndef MIVQ_CS_D64_WAVES
+#define MIVQ_CS_D64_WAVES 16
+#endif
+#ifndef MIVQ_CS_D96_WAVES
+#define MIVQ_CS_D96_WAVES 12
+#endif
+    int nw_launch = NW, smem_launch = smem;
     if constexpr (KS == 6) {
-        if (dsub == 96) kern = pq_encode_cs_kernel<6, 3, V, 96>;
+        if (dsub == 96) {
+            kern = pq_encode_cs_kernel<6, 3, V, 96, MIVQ_CS_D96_WAVES>;
+            nw_launch = MIVQ_CS_D96_WAVES;
+            smem_launch = smem + (MIVQ_CS_D96_WAVES - NW) * 32 * (32 * KS + 16);
+        }
     }
-    hipError_t e = hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, smem);
+    if constexpr (KS == 4) {  // D = 1024, M = 16 (BASELINE config #5)
+        if (dsub == 64) {
+            kern = pq_encode_cs_kernel<4, 1, V, 64, MIVQ_CS_D64_WAVES>;
+            nw_launch = MIVQ_CS_D64_WAVES;
+            smem_launch = smem + (MIVQ_CS_D64_WAVES - NW) * 32 * (32 * KS + 16);
+        }
+    }
+    hipError_t e = hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, smem_launch);
     if (e != hipSuccess) return e;
     const int cus = device_cus();
-    const int64_t chunks = pick_chunks(n, d, M, cus, NW);
+    const int64_t chunks = pick_chunks(n, d, M, cus, nw_launch);
     const int64_t R = align_up(ceil_div(n, chunks), (int64_t)32);
     const int64_t grid = ceil_div(n, R) * M;
     // V & (1 << 20): the round-1 resolve (pair window in the pair kernel, separate full-item
     // and pair kernels), kept for A/B profiling
     constexpr bool legacy = (V & (1 << 20)) != 0;
     const float2* pdw = legacy ? nullptr : static_cast<const float2*>(pd);
-    hipLaunchKernelGGL(kern, dim3((unsigned)grid), dim3(NW * 64), smem, st, x, n, d, M, dsub, R, C, cn,
+    hipLaunchKernelGGL(kern, dim3((unsigned)grid), dim3(nw_launch * 64), smem_launch, st, x, n, d, M, dsub, R, C, cn,
                        static_cast<const half8*>(img), hinit, static_cast<const float4*>(bnd), codesT,
                        static_cast<uint2*>(items), static_cast<int2*>(counts), static_cast<float2*>(pinfo), pdw,
                        static_cast<const float4*>(bnd2));
@@ -1727,8 +1745,9 @@ hipError_t launch_pq_encode_cs_v(const float* x, int64_t n, int d, int M, int ds
     if constexpr (!legacy) {
         constexpr int msmem = merged_smem_bytes<KS>();
         static_assert(msmem <= 160 * 1024, "merged resolve LDS");
-        auto mkern = (KS == 6 && dsub == 96) ? pq_resolve_merged_kernel<KS, (KS == 6 ? 96 : 0), V>
-                                             : pq_resolve_merged_kernel<KS, 0, V>;
+        auto mkern = (KS == 6 && dsub == 96)   ? pq_resolve_merged_kernel<KS, (KS == 6 ? 96 : 0), V>
+                     : (KS == 4 && dsub == 64) ? pq_resolve_merged_kernel<KS, (KS == 4 ? 64 : 0), V>
+                                               : pq_resolve_merged_kernel<KS, 0, V>;
         e = hipFuncSetAttribute((const void*)mkern, hipFuncAttributeMaxDynamicSharedMemorySize, msmem);
         if (e != hipSuccess) return e;
         hipLaunchKernelGGL(mkern, dim3((unsigned)grid), dim3(kMWaves * 64), msmem, st, x, n, d, M, dsub, R, C, cn,

@@ -292,6 +292,32 @@ def test_sq_vector_path_equals_generic(dev, bits):
         np.testing.assert_array_equal(_h(a), _h(b)[:, :d])
 
 
+@pytest.mark.parametrize("bits", [8, 16])
+def test_sq_vector_path_division_at_rounding_boundaries(dev, bits):
+    """The vector path divides through a correctly rounded reciprocal plus one residual
+    correction (sq.hip: div_rn_rcp); the generic kernel uses the IEEE division.  Elements are
+    placed so that (x - lo) / den * L lands within a few ulps of a rounding boundary k + 1/2,
+    where a quotient one ulp off flips the code: both paths must agree on every element, over
+    den magnitudes 2^-60..2^60 and both signs of x - lo."""
+    from haag_vq import _native
+
+    n, d = 100_000, 64
+    L = (1 << bits) - 1
+    g = torch.Generator(device=dev).manual_seed(17 + bits)
+    den = torch.logspace(-18, 18, d, device=dev, dtype=torch.float64)
+    lo = torch.randn((d,), device=dev, generator=g, dtype=torch.float64) * den
+    k = torch.randint(0, L, (n, d), device=dev, generator=g).double()
+    t = (k + 0.5) / L + torch.randint(-3, 4, (n, d), device=dev, generator=g).double() * 2.0 ** -24 / L
+    X = (lo + den * t).float()
+    X[1::2] = (lo - den * t[1::2]).float()  # negative quotients (clipped by the cast)
+    lo32, den32 = lo.float().contiguous(), den.float().contiguous()
+    Xp = torch.cat([X, torch.zeros((n, 1), device=dev)], 1).contiguous()
+    a = _native.sq_encode(X.contiguous(), lo32, den32, bits)
+    b = _native.sq_encode(Xp, torch.cat([lo32, lo32[:1]]).contiguous(), torch.cat([den32, den32[:1]]).contiguous(),
+                          bits)
+    np.testing.assert_array_equal(_h(a), _h(b)[:, :d])
+
+
 @pytest.mark.parametrize("n,d", [(500, 1024), (333, 3072), (77, 37)])
 @pytest.mark.parametrize("metric", [1, 0])
 def test_rabitq_parity(dev, oracle, n, d, metric):

@@ -37,7 +37,15 @@ def _run(dev, X, C, A):
     Y = _native.opq_rotate_prepared(X, oprep)
     lut = _native.adc_lut(X[:64], C, 8)
     dists, ids = _native.adc_search(lut, codes, 10, 8)
+    # device addresses of this call's buffers (printed on a mismatch: which live buffers of
+    # the other thread sat next to the corrupted one)
+    _ADDR.append((threading.get_ident(), {k: (t.data_ptr(), t.numel() * t.element_size())
+                                          for k, t in (("codes", codes), ("Y", Y), ("lut", lut), ("dists", dists),
+                                                       ("ids", ids), ("prep", prep), ("oprep", oprep))}))
     return {"codes": codes, "Y": Y, "lut": lut, "ids": ids, "dists": dists}
+
+
+_ADDR = []
 
 
 def _diff(name, got, want):
@@ -45,8 +53,16 @@ def _diff(name, got, want):
         bad = (got != want) & ~(torch.isnan(got) & torch.isnan(want))
     else:
         bad = got != want
-    at = bad.nonzero()[:4].tolist()
-    return f"{name}: {int(bad.sum())} of {got.numel()} differ, first at {at}"
+    flat = bad.reshape(-1).nonzero().reshape(-1).tolist()
+    runs, start = [], None  # differing elements as runs of flat indices (a corrupted span shows as one)
+    for j, v in enumerate(flat):
+        if start is None:
+            start = v
+        if j + 1 == len(flat) or flat[j + 1] != v + 1:
+            runs.append((start, v + 1))
+            start = None
+    return (f"{name}: {int(bad.sum())} of {got.numel()} differ, first at {bad.nonzero()[:4].tolist()}, "
+            f"flat runs {runs[:6]} (element size {got.element_size()} B)")
 
 
 @pytest.mark.parametrize("trial", range(2))
@@ -79,7 +95,7 @@ def test_two_threads_two_streams_match_serial(dev, trial):
     assert not errors, errors
     diffs = [f"input {i} " + _diff(k, results[i][k], ref[i][k])
              for i in range(2) for k in ref[i] if not torch.equal(results[i][k], ref[i][k])]
-    assert not diffs, diffs
+    assert not diffs, (diffs, _ADDR[-10:])
 
 
 def test_error_message_is_per_thread(dev):

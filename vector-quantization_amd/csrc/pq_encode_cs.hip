@@ -1708,6 +1708,9 @@ hipError_t launch_pq_encode_cs_v(const float* x, int64_t n, int d, int M, int ds
 #ifndef MIVQ_CS_D64_WAVES
 #define MIVQ_CS_D64_WAVES 16
 #endif
+#ifndef MIVQ_CS_D48_WAVES
+#define MIVQ_CS_D48_WAVES 16
+#endif
 #ifndef MIVQ_CS_D96_WAVES
 #define MIVQ_CS_D96_WAVES 12
 #endif
@@ -1717,6 +1720,13 @@ hipError_t launch_pq_encode_cs_v(const float* x, int64_t n, int d, int M, int ds
             kern = pq_encode_cs_kernel<6, 3, V, 96, MIVQ_CS_D96_WAVES>;
             nw_launch = MIVQ_CS_D96_WAVES;
             smem_launch = smem + (MIVQ_CS_D96_WAVES - NW) * 32 * (32 * KS + 16);
+        }
+    }
+    if constexpr (KS == 3) {  // D = 1536, M = 32 (the OPQ32 / PQ32 shape of BASELINE config #3)
+        if (dsub == 48) {
+            kern = pq_encode_cs_kernel<3, 3, V, 48, MIVQ_CS_D48_WAVES>;
+            nw_launch = MIVQ_CS_D48_WAVES;
+            smem_launch = smem + (MIVQ_CS_D48_WAVES - NW) * 32 * (32 * KS + 16);
         }
     }
     if constexpr (KS == 4) {  // D = 1024, M = 16 (BASELINE config #5)
@@ -1747,6 +1757,7 @@ hipError_t launch_pq_encode_cs_v(const float* x, int64_t n, int d, int M, int ds
         static_assert(msmem <= 160 * 1024, "merged resolve LDS");
         auto mkern = (KS == 6 && dsub == 96)   ? pq_resolve_merged_kernel<KS, (KS == 6 ? 96 : 0), V>
                      : (KS == 4 && dsub == 64) ? pq_resolve_merged_kernel<KS, (KS == 4 ? 64 : 0), V>
+                     : (KS == 3 && dsub == 48) ? pq_resolve_merged_kernel<KS, (KS == 3 ? 48 : 0), V>
                                                : pq_resolve_merged_kernel<KS, 0, V>;
         e = hipFuncSetAttribute((const void*)mkern, hipFuncAttributeMaxDynamicSharedMemorySize, msmem);
         if (e != hipSuccess) return e;

@@ -62,8 +62,10 @@ def _diff(name, got, want):
         if j + 1 == len(flat) or flat[j + 1] != v + 1:
             runs.append((start, v + 1))
             start = None
+    g, w = got.reshape(-1), want.reshape(-1)
+    vals = [(g[a:a + 4].tolist(), w[a:a + 4].tolist()) for a, _ in runs[:2]]  # (got, want) at two runs
     return (f"{name}: {int(bad.sum())} of {got.numel()} differ, first at {bad.nonzero()[:4].tolist()}, "
-            f"flat runs {runs[:6]} (element size {got.element_size()} B)")
+            f"flat runs {runs[:6]} (element size {got.element_size()} B), values (got, want) {vals}")
 
 
 # Open issue: in about one trial in three, when this test runs after the other
@@ -82,6 +84,7 @@ def test_two_threads_two_streams_match_serial(dev, trial):
     torch.cuda.synchronize()
 
     results = [None, None]
+    dev_out = [None, None]
     errors = []
 
     def worker(i):
@@ -91,6 +94,10 @@ def test_two_threads_two_streams_match_serial(dev, trial):
                 out = None
                 for _ in range(4):
                     out = _run(dev, *inputs[i])
+                # device-side copies (compared on the device below) and host copies made by
+                # both threads at the same time (pageable D2H), kept apart so that a mismatch
+                # names where it arises: the kernels' outputs or the concurrent host copies
+                dev_out[i] = {k: t.clone() for k, t in out.items()}
                 s.synchronize()
                 results[i] = {k: t.cpu() for k, t in out.items()}
         except Exception as e:  # surfaced below
@@ -102,13 +109,17 @@ def test_two_threads_two_streams_match_serial(dev, trial):
     for t in th:
         t.join(timeout=300)
     assert not errors, errors
-    diffs = [f"input {i} " + _diff(k, results[i][k], ref[i][k])
+    torch.cuda.synchronize()
+    dev_diffs = [f"input {i} device " + _diff(k, dev_out[i][k].cpu(), ref[i][k])
+                 for i in range(2) for k in ref[i] if not torch.equal(dev_out[i][k].cpu(), ref[i][k])]
+    diffs = dev_diffs + [f"input {i} " + _diff(k, results[i][k], ref[i][k])
              for i in range(2) for k in ref[i] if not torch.equal(results[i][k], ref[i][k])]
     if diffs and os.environ.get("MIVQ_CONC_DIAG"):
         import json
 
         with open(os.environ["MIVQ_CONC_DIAG"], "a") as f:
-            f.write(json.dumps({"trial": trial, "diffs": diffs, "addr": _ADDR[-12:]}) + "\n")
+            f.write(json.dumps({"trial": trial, "device_diffs": dev_diffs, "diffs": diffs,
+                                "addr": _ADDR[-12:]}) + "\n")
     assert not diffs, (diffs, _ADDR[-10:])
 
 

@@ -117,6 +117,15 @@ def test_two_threads_two_streams_match_serial(dev, trial):
     if diffs and os.environ.get("MIVQ_CONC_DIAG"):
         import json
 
+        # which side is wrong: both LUTs against a torch fp32 LUT (different summation order:
+        # ~1e-7 relative, far below the ~1e-3 of the differing spans)
+        for i in range(2):
+            X, C, _ = inputs[i]
+            q = X[:64].reshape(64, 8, 1, 96)
+            tl = ((q - C.unsqueeze(0)) ** 2).sum(-1).cpu()
+            dev_diffs.append(f"input {i} max|ref-torch| {float((ref[i]['lut'] - tl).abs().max()):.3g} "
+                             f"max|conc-torch| {float((dev_out[i]['lut'].cpu() - tl).abs().max()):.3g}")
+
         with open(os.environ["MIVQ_CONC_DIAG"], "a") as f:
             f.write(json.dumps({"trial": trial, "device_diffs": dev_diffs, "diffs": diffs,
                                 "addr": _ADDR[-12:]}) + "\n")

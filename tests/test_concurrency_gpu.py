@@ -83,6 +83,8 @@ def test_two_threads_two_streams_match_serial(dev, trial):
     ref = [{k: t.cpu() for k, t in _run(dev, *inp).items()} for inp in inputs]
     torch.cuda.synchronize()
 
+    saved = [(inp[0][:64].clone(), inp[1].clone()) for inp in inputs]  # inputs intact afterwards?
+    torch.cuda.synchronize()
     results = [None, None]
     dev_out = [None, None]
     errors = []
@@ -123,6 +125,8 @@ def test_two_threads_two_streams_match_serial(dev, trial):
             X, C, _ = inputs[i]
             q = X[:64].reshape(64, 8, 1, 96)
             tl = ((q - C.unsqueeze(0)) ** 2).sum(-1).cpu()
+            dev_diffs.append(f"input {i} queries changed {int((X[:64] != saved[i][0]).sum())} "
+                             f"centroids changed {int((C != saved[i][1]).sum())}")
             dev_diffs.append(f"input {i} max|ref-torch| {float((ref[i]['lut'] - tl).abs().max()):.3g} "
                              f"max|conc-torch| {float((dev_out[i]['lut'].cpu() - tl).abs().max()):.3g}")
 

@@ -110,8 +110,7 @@ int mivq_opq_rotate(const float* x, int64_t n, int32_t d, const float* A, int32_
  * images (prep: mivq_opq_prep_bytes(d) bytes, 16-byte aligned; 0 when d % 8 != 0), and
  * mivq_opq_rotate_prepared computes y = x . op(A) as x_hi b_hi + x_hi b_lo + x_lo b_hi with
  * per-row power-of-two scales of x.  Workspace (16-byte aligned):
- * mivq_opq_rotate_workspace_bytes(n, d) = the row scales (4 n B) plus the f16 hi / lo planes of
- * at most 2^20 rows of x (4 d min(n, 2^20) B); larger n is rotated in chunks of 2^20 rows. */
+ * mivq_opq_rotate_workspace_bytes(n, d) = the row scales (4 n B, rounded up to 256 B). */
 size_t mivq_opq_prep_bytes(int32_t d);
 int mivq_opq_prepare(const float* A, int32_t d, int32_t transpose, void* prep, void* stream);
 size_t mivq_opq_rotate_workspace_bytes(int64_t n, int32_t d);

@@ -68,16 +68,11 @@ def _diff(name, got, want):
             f"flat runs {runs[:6]} (element size {got.element_size()} B), values (got, want) {vals}")
 
 
-# Open issue: in about one trial in three, when this test runs after the other
-# GPU tests in the same process, 64-byte spans of adc_lut's output -- always the stores of
-# lanes 48..63 of a wave -- hold values that differ from the serial run, while every other
-# output (codes, rotation) is identical and the two threads' buffers do not overlap
-# (addresses recorded in the failure message).  Later also seen with this test alone in a fresh
-# process; the inputs stay intact in memory and the serial LUT matches a torch fp32 LUT.
-# The LUT kernel's 16-B centroid loads were replaced by dword loads, and since then 0 of 18 trials
-# have failed (1-5 of 8 before).  The root cause is unknown, so the test is still a non-strict xfail; the failure
-# details are appended to $MIVQ_CONC_DIAG when set.
-@pytest.mark.xfail(strict=False, reason="intermittent adc_lut mismatch under two-stream concurrency, mitigated by dword loads (DESIGN §8)")
+# Round 2 saw 64-byte spans of adc_lut's output (lanes 48..63 of a wave) differ here in 1-5 of
+# 8 trials.  Cause (tools/probes/lut_stress.hip): the LDS-DMA OPQ GEMM then used
+# for d % 32 == 0, resident on the same CUs, corrupted lanes 48..63 of the LUT kernel's packed
+# fp32 instructions.  The library no longer issues LDS DMA; this test is strict again, and
+# test_lut_beside_opq_rotation below targets the exact overlap with many launches.
 @pytest.mark.parametrize("trial", range(int(os.environ.get("MIVQ_CONC_TRIALS", "2"))))
 def test_two_threads_two_streams_match_serial(dev, trial):
     inputs = [_work(dev, s) for s in (1, 2)]
@@ -189,3 +184,34 @@ def test_pq_prepare_is_byte_deterministic(dev):
     del junk
     b = _native.pq_prepare(C, 8).cpu()
     assert torch.equal(a, b)
+
+
+def test_lut_beside_opq_rotation(dev):
+    """The overlap that exposed round 2's defect, many times over: stream B rotates a 400k x 768
+    block (the prepared split-f16 GEMM, ~2 ms) while stream A computes the same ADC LUT 16
+    times; every LUT must equal the one computed alone.  With the LDS-DMA GEMM about one LUT
+    launch in six came out wrong (profiles/r03_s1_lut_stress*.log), so 20 rounds x 16 launches
+    would all but surely have caught it."""
+    from haag_vq import _native
+
+    g = torch.Generator(device=dev).manual_seed(7)
+    X = torch.randn((400_000, 768), device=dev, generator=g)
+    C = torch.randn((8, 256, 96), device=dev, generator=g)
+    A, _ = torch.linalg.qr(torch.randn((768, 768), device=dev, generator=g, dtype=torch.float64))
+    oprep = _native.opq_prepare(A.float().contiguous(), False)
+    Q = X[:64].contiguous()
+    ref = _native.adc_lut(Q, C, 8)
+    torch.cuda.synchronize()
+    sa, sb = torch.cuda.Stream(device=dev), torch.cuda.Stream(device=dev)
+    bad = []
+    for rnd in range(20):
+        with torch.cuda.stream(sb):
+            _native.opq_rotate_prepared(X, oprep)
+        with torch.cuda.stream(sa):
+            luts = [_native.adc_lut(Q, C, 8) for _ in range(16)]
+        torch.cuda.synchronize()
+        for j, lut in enumerate(luts):
+            if not torch.equal(lut, ref):
+                idx = (lut != ref).reshape(-1).nonzero().reshape(-1)
+                bad.append((rnd, j, int(idx.numel()), idx[:4].tolist()))
+    assert not bad, bad

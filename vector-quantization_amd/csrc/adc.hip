@@ -66,15 +66,24 @@ __global__ __launch_bounds__(256) void adc_lut_kernel(const float* __restrict__ 
             }
         }
     };
-    // Dword loads of the centroid row.  A 16-B (v4f) load form was used until round 2: under
-    // two-stream concurrency it intermittently returned wrong data to lanes 48..63 of a wave
-    // (inputs intact in memory, serial runs exact; tests/test_concurrency_gpu.py);
-    // with dword loads 0 of 8 concurrent trials differed against 1-5 of 8 before.
-    for (int t0 = 0; t0 < dsub; t0 += 4) {
-        const int nt = min(4, dsub - t0);
-        const float c0 = c[t0], c1 = nt > 1 ? c[t0 + 1] : 0.0f;
-        const float c2 = nt > 2 ? c[t0 + 2] : 0.0f, c3 = nt > 3 ? c[t0 + 3] : 0.0f;
-        step(c0, c1, c2, c3, t0, nt);
+    if ((dsub & 3) == 0) {
+        // 16-B loads of the centroid row, the next one in flight while this one is used.  (Round
+        // 2 replaced these by dword loads while chasing a two-stream mismatch in lanes 48..63;
+        // the cause was the LDS-DMA OPQ GEMM on the other stream corrupting packed-fp32 results,
+        // since removed from the library: DESIGN §8.  The load form was never involved.)
+        v4f cur = *reinterpret_cast<const v4f*>(c);
+        for (int t0 = 0; t0 < dsub; t0 += 4) {
+            const v4f nxt = (t0 + 4 < dsub) ? *reinterpret_cast<const v4f*>(c + t0 + 4) : cur;
+            step(cur.x, cur.y, cur.z, cur.w, t0, 4);
+            cur = nxt;
+        }
+    } else {
+        for (int t0 = 0; t0 < dsub; t0 += 4) {
+            const int nt = min(4, dsub - t0);
+            const float c0 = c[t0], c1 = nt > 1 ? c[t0 + 1] : 0.0f;
+            const float c2 = nt > 2 ? c[t0 + 2] : 0.0f, c3 = nt > 3 ? c[t0 + 3] : 0.0f;
+            step(c0, c1, c2, c3, t0, nt);
+        }
     }
 #pragma unroll
     for (int qq = 0; qq < kLutQ; ++qq)

@@ -17,15 +17,16 @@
 //    GEMM has (tests/test_opq_gpu.py checks 1e-5 of ||x|| ||a|| against fp64).  Three
 //    v_mfma_f32_32x32x16_f16 per 32x32x16 block = 3 x 1/16 of the fp32-MFMA cost per flop.
 //    mivq_opq_prepare builds the hi / lo images of B = op(A) once per matrix ([col][k] rows,
-//    scaled).  d % 32 == 0 (the shapes that matter): opq_split_x_kernel writes x's row scales
-//    and hi / lo planes (one pass, chunks of 2^20 rows in the workspace), then
-//    opq_glds_gemm_kernel: 256 x 256 tiles per 512-thread workgroup (8 waves of 64 x 128 =
-//    2 x 4 MFMA blocks), all four planes global -> LDS by global_load_lds_dwordx4 (no register
-//    staging, chunk-swizzled unpadded rows: conflict-free fragment reads), two 64-KiB stages.
-//    Other d: opq_row_scale_kernel + opq_split_gemm_kernel, which splits x itself while staging
-//    (register-staged, 80-B padded rows, 256 x 256 or 128 x 128 tiles).  Both: XCD-aware tile
-//    order (the workgroups one XCD runs cover consecutive tiles, so the column tiles of a row
-//    block share its L2) and an epilogue that goes out through LDS as 16-B row stores.
+//    scaled); opq_row_scale_kernel computes x's row scales; opq_split_gemm_kernel splits x
+//    while staging it (register-staged, 80-B padded rows, 256 x 256 or 128 x 128 tiles,
+//    XCD-aware tile order so the column tiles of a row block share one L2, epilogue through
+//    LDS as 16-B row stores).
+//    No LDS DMA (global_load_lds_*): round 2's DMA-staged GEMM, while resident next to another
+//    kernel's waves, corrupted lanes 48..63 of their packed-fp32 VALU results (v_pk_add_f32 /
+//    v_pk_fma_f32 on LDS-loaded operands); a synthetic kernel that only overlaps LDS DMA with
+//    MFMAs does the same, and neither does it without the MFMAs or without the DMA
+//    (tools/probes/lut_stress.hip).  The library must not corrupt kernels it runs
+//    beside (its own, torch's), so every shape takes the register-staged path.
 // 2. opq_gemm_kernel (mivq_opq_rotate, no preparation, any d): plain fp32 MFMA
 //    (v_mfma_f32_32x32x2_f32), 128 x 128 tiles, BK = 16 slices staged through LDS.
 #include <math.h>
@@ -159,45 +160,6 @@ __global__ __launch_bounds__(256) void opq_row_scale_kernel(const float* __restr
     for (int o = 32; o > 0; o >>= 1) m = fmaxf(m, __shfl_xor(m, o));
     bad = __any(bad);
     if (l == 0) rs[row] = bad ? 1.0f : pow2_scale(m);
-}
-
-// Row scale and split of x in one pass (one wave per row): rs[row] = s_x, and the f16 planes
-// xs[0][row][k] = hi, xs[1][row][k] = lo of s_x x[row][k] (the GEMM then stages them by plain
-// 16-B copies instead of re-splitting x once per column tile).
-__global__ __launch_bounds__(256) void opq_split_x_kernel(const float* __restrict__ x, int64_t n, int d,
-                                                          float* __restrict__ rs, _Float16* __restrict__ xs) {
-    const int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
-    const int l = threadIdx.x & 63;
-    if (row >= n) return;
-    const float4* xr = reinterpret_cast<const float4*>(x + row * d);
-    const int q = d >> 2;  // d % 8 == 0
-    float m = 0.0f;
-    bool bad = false;
-    for (int k = l; k < q; k += 64) {
-        const float4 v = xr[k];
-        bad |= !isfinite(v.x) || !isfinite(v.y) || !isfinite(v.z) || !isfinite(v.w);
-        m = fmaxf(m, fmaxf(fmaxf(fabsf(v.x), fabsf(v.y)), fmaxf(fabsf(v.z), fabsf(v.w))));
-    }
-    for (int o = 32; o > 0; o >>= 1) m = fmaxf(m, __shfl_xor(m, o));
-    bad = __any(bad);
-    const float s = bad ? 1.0f : pow2_scale(m);
-    if (l == 0) rs[row] = s;
-    half4* ph = reinterpret_cast<half4*>(xs + row * d);
-    half4* pl = reinterpret_cast<half4*>(xs + (n + row) * d);
-    for (int k = l; k < q; k += 64) {
-        const float4 v = xr[k];
-        const float w[4] = {v.x * s, v.y * s, v.z * s, v.w * s};
-        half4 h, lo;
-#pragma unroll
-        for (int t = 0; t < 4; ++t) {
-            _Float16 a, b;
-            split2(w[t], a, b);
-            h[t] = a;
-            lo[t] = b;
-        }
-        ph[k] = h;
-        pl[k] = lo;
-    }
 }
 
 // max |A| over the whole matrix -> header {s_b, 1 / s_b} of the prepared image (one workgroup).
@@ -409,148 +371,6 @@ __global__ __launch_bounds__(WR * WC * 64) void opq_split_gemm_kernel(const floa
     store_tile<RB, CB>(acc, smem, w, l, r0 + wr * RB * 32, c0 + wc * CB * 32, n, d, rs, hdr[1], y);
 }
 
-// LDS-DMA variant (x pre-split): all four planes (x hi, x lo, B hi, B lo) go global -> LDS
-// with global_load_lds_dwordx4, no register staging.  One wave-instruction writes 1 KiB of one
-// plane contiguously (the LDS destination is lane-linear), so the planes are unpadded rows of
-// 2 KSTEP bytes whose 16-B chunks are permuted through the SOURCE address (64-B rows:
-// c ^ ((r >> 2) & 3); 32-B rows: c ^ ((r >> 3) & 1)): the rows one 16-lane group of a fragment
-// ds_read_b128 touches then land on 16 distinct chunk slots of the bank row.
-// NS stages in a ring: the loads run NS - 1 K steps ahead; each step waits (counted vmcnt) for
-// its own stage only, then one raw s_barrier both publishes it and retires the slot the next
-// load overwrites (no __syncthreads: its fence would drain every load in flight).
-template <int KSTEP, int NS>
-struct GldsCfg {
-    static constexpr int ROWB = 2 * KSTEP;          // bytes per plane row
-    static constexpr int PL = 256 * ROWB;           // one plane of one stage
-    static constexpr int STAGE = 4 * PL;            // x hi, x lo, B hi, B lo
-    static constexpr int SMEM = NS * STAGE;
-    static constexpr int CPR = ROWB / 16;           // 16-B chunks per row
-    static constexpr int RPI = 64 / CPR;            // rows per DMA instruction
-    static constexpr int IPW = STAGE / 1024 / 8;    // DMA instructions per wave per stage
-    static_assert(SMEM <= 160 * 1024 && IPW * (NS - 1) <= 60, "glds ring");
-};
-
-template <int ROWB>
-__device__ __forceinline__ int glds_swz(int row) { return ROWB == 64 ? ((row >> 2) & 3) : ((row >> 3) & 1); }
-
-typedef __attribute__((address_space(3))) void lds_void;
-
-template <int KSTEP, int NS>
-__global__ __launch_bounds__(512) void opq_glds_gemm_kernel(int64_t n, int d, const _Float16* __restrict__ xsp,
-                                                            const float* __restrict__ rs,
-                                                            const _Float16* __restrict__ bimg,
-                                                            const float* __restrict__ hdr, float* __restrict__ y,
-                                                            int64_t ctiles) {
-    using G = GldsCfg<KSTEP, NS>;
-    constexpr int WC = 2, RB = 2, CB = 4, TM = 256, TN = 256;
-    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-    const int tid = threadIdx.x, l = tid & 63, w = tid >> 6;
-    const int wr = w / WC, wc = w % WC;
-    const int64_t t = xcd_tile(blockIdx.x, gridDim.x);
-    const int64_t r0 = (t / ctiles) * TM;
-    const int c0 = (int)(t % ctiles) * TN;
-    const int64_t dd = (int64_t)d * d;
-
-    // this lane's source for each of the wave's IPW DMA instructions per stage: instruction
-    // q = IPW w + i covers plane q / (PL / 1024), rows RPI (q % (PL / 1024)) + [0, RPI); lane l
-    // -> row + l / CPR, physical chunk l % CPR holding logical chunk (l % CPR) ^ swz(row).
-    // Rows past n / columns past d read row n - 1 / column d - 1 (their outputs are dropped).
-    constexpr int QPP = G::PL / 1024;  // instructions per plane
-    const _Float16* src[G::IPW];
-#pragma unroll
-    for (int i = 0; i < G::IPW; ++i) {
-        const int q = G::IPW * w + i, pl = q / QPP;
-        const int row = G::RPI * (q % QPP) + l / G::CPR;
-        const int c = (l % G::CPR) ^ glds_swz<G::ROWB>(row);
-        if (pl < 2) {
-            const int64_t gr = min(r0 + row, n - 1);
-            src[i] = xsp + ((int64_t)pl * n + gr) * d + 8 * c;
-        } else {
-            const int64_t gc = min((int64_t)c0 + row, (int64_t)d - 1);
-            src[i] = bimg + (int64_t)(pl - 2) * dd + gc * d + 8 * c;
-        }
-    }
-    auto issue = [&](int step, int slot) __attribute__((always_inline)) {
-#pragma unroll
-        for (int i = 0; i < G::IPW; ++i) {
-            const int q = G::IPW * w + i;
-            lds_void* dst = (lds_void*)(smem + slot * G::STAGE + (q / QPP) * G::PL + (q % QPP) * 1024);
-            __builtin_amdgcn_global_load_lds((const void*)(src[i] + step * KSTEP), dst, 16, 0, 0);
-        }
-    };
-
-    floatx16 acc[RB][CB];
-#pragma unroll
-    for (int a = 0; a < RB; ++a)
-#pragma unroll
-        for (int b = 0; b < CB; ++b)
-#pragma unroll
-            for (int e = 0; e < 16; ++e) acc[a][b][e] = 0.0f;
-
-    const int fr = l & 31, fh = l >> 5;
-    auto frag = [&](const unsigned char* plane, int row, int kk) __attribute__((always_inline)) {
-        const int c = (2 * kk + fh) ^ glds_swz<G::ROWB>(row);
-        return *reinterpret_cast<const half8*>(plane + row * G::ROWB + 16 * c);
-    };
-    const int nsteps = d / KSTEP;
-#pragma unroll
-    for (int st = 0; st < NS - 1; ++st)
-        if (st < nsteps) issue(st, st);
-    for (int s = 0; s < nsteps; ++s) {
-        // stage s landed: the loads issued after it (steps s + 1 .. s + NS - 2) may stay in flight
-        if (nsteps - 1 - s >= NS - 2) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(G::IPW * (NS - 2)) : "memory");
-        else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        __builtin_amdgcn_s_barrier();
-        if (s + NS - 1 < nsteps) issue(s + NS - 1, (s + NS - 1) % NS);
-        const unsigned char* cur = smem + (s % NS) * G::STAGE;
-#pragma unroll
-        for (int kk = 0; kk < KSTEP / 16; ++kk) {
-            half8 ah[RB], al[RB], bh[CB], bl[CB];
-#pragma unroll
-            for (int i = 0; i < RB; ++i) {
-                const int row = wr * RB * 32 + i * 32 + fr;
-                ah[i] = frag(cur, row, kk);
-                al[i] = frag(cur + G::PL, row, kk);
-            }
-#pragma unroll
-            for (int j = 0; j < CB; ++j) {
-                const int row = wc * CB * 32 + j * 32 + fr;
-                bh[j] = frag(cur + 2 * G::PL, row, kk);
-                bl[j] = frag(cur + 3 * G::PL, row, kk);
-            }
-#pragma unroll
-            for (int a = 0; a < RB; ++a)
-#pragma unroll
-                for (int b = 0; b < CB; ++b) acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x16_f16(al[a], bh[b], acc[a][b], 0, 0, 0);
-#pragma unroll
-            for (int a = 0; a < RB; ++a)
-#pragma unroll
-                for (int b = 0; b < CB; ++b) acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[a], bl[b], acc[a][b], 0, 0, 0);
-#pragma unroll
-            for (int a = 0; a < RB; ++a)
-#pragma unroll
-                for (int b = 0; b < CB; ++b) acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[a], bh[b], acc[a][b], 0, 0, 0);
-        }
-    }
-    // epilogue (the staging buffers are reused: every wave must be done with them)
-    __syncthreads();
-    store_tile<RB, CB>(acc, smem, w, l, r0 + wr * RB * 32, c0 + wc * CB * 32, n, d, rs, hdr[1], y);
-}
-
-template <int KSTEP, int NS>
-int launch_glds(const _Float16* xsp, int64_t n, int d, const float* rs, const _Float16* bimg, const float* hdr,
-                float* y, hipStream_t st) {
-    using G = GldsCfg<KSTEP, NS>;
-    auto kern = opq_glds_gemm_kernel<KSTEP, NS>;
-    hipError_t e = hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, G::SMEM);
-    if (e != hipSuccess) return set_error(MIVQ_ERR_HIP, "opq_glds_gemm: %s", hipGetErrorString(e));
-    const int64_t ct = ceil_div(d, 256), tiles = ceil_div(n, 256) * ct;
-    MIVQ_REQUIRE(tiles < ((int64_t)1 << 31), MIVQ_ERR_UNSUPPORTED, "opq_rotate_prepared: n=%lld too large for one call",
-                 (long long)n);
-    hipLaunchKernelGGL(kern, dim3((unsigned)tiles), dim3(512), G::SMEM, st, n, d, xsp, rs, bimg, hdr, y, ct);
-    return check_launch("opq_glds_gemm");
-}
-
 template <class T, int WR, int WC, int RB, int CB>
 int launch_split(const float* x, int64_t n, int d, const float* rs, const _Float16* bimg, const float* hdr, float* y,
                  hipStream_t st) {
@@ -601,13 +421,12 @@ extern "C" int mivq_opq_prepare(const float* A, int32_t d, int32_t transpose, vo
     return check_launch("opq_split_b");
 }
 
-// Rows per GEMM launch: the f16 planes of x (4 B per element) live in the workspace for one
-// chunk at a time.
+// Rows per GEMM launch (keeps the tile count of one launch far below 2^31).
 constexpr int64_t kOpqChunk = (int64_t)1 << 20;
 
 extern "C" size_t mivq_opq_rotate_workspace_bytes(int64_t n, int32_t d) {
     if (n <= 0 || d <= 0) return 0;
-    return align_up((size_t)n * sizeof(float), 256) + align_up((size_t)std::min(n, kOpqChunk) * d * 4, 256);
+    return align_up((size_t)n * sizeof(float), 256);  // the row scales
 }
 
 extern "C" int mivq_opq_rotate_prepared(const float* x, int64_t n, int32_t d, const void* prep, void* workspace,
@@ -625,34 +444,19 @@ extern "C" int mivq_opq_rotate_prepared(const float* x, int64_t n, int32_t d, co
                  "opq_rotate_prepared: workspace must be 16-byte aligned");
     hipStream_t st = as_stream(stream);
     float* rs = static_cast<float*>(workspace);
-    _Float16* xsp = reinterpret_cast<_Float16*>(static_cast<unsigned char*>(workspace) +
-                                                align_up((size_t)n * sizeof(float), 256));
     const float* hdr = static_cast<const float*>(prep);
     const _Float16* bimg = reinterpret_cast<const _Float16*>(static_cast<const unsigned char*>(prep) + 256);
-    // d % 32 == 0 with at least one 256 x 256 tile: x split once into its f16 planes, then the
-    // LDS-DMA GEMM; otherwise row scales only and the register-staged GEMM splits x itself
-    const bool dma = d % 32 == 0 && d >= 256;
     for (int64_t c0 = 0; c0 < n; c0 += kOpqChunk) {
         const int64_t cn = std::min(kOpqChunk, n - c0);
         const float* xc = x + c0 * d;
         float* yc = y + c0 * d;
-        int rc;
-        if (dma && cn >= 256) {
-            hipLaunchKernelGGL(opq_split_x_kernel, dim3((unsigned)ceil_div(cn, 4)), dim3(256), 0, st, xc, cn, d,
-                               rs + c0, xsp);
-            rc = check_launch("opq_split_x");
-            if (rc) return rc;
-            rc = launch_glds<32, 2>(xsp, cn, d, rs + c0, bimg, hdr, yc, st);
-        } else {
-            hipLaunchKernelGGL(opq_row_scale_kernel, dim3((unsigned)ceil_div(cn, 4)), dim3(256), 0, st, xc, cn, d,
-                               rs + c0);
-            rc = check_launch("opq_row_scale");
-            if (rc) return rc;
-            // 256 x 256 tiles (512 threads, 160 KiB) wherever a row block spans at least one
-            // such tile; the 128 x 128 kernel for narrow matrices
-            rc = (d >= 256 && cn >= 256) ? launch_split<TileL, 4, 2, 2, 4>(xc, cn, d, rs + c0, bimg, hdr, yc, st)
-                                         : launch_split<TileS, 2, 2, 2, 2>(xc, cn, d, rs + c0, bimg, hdr, yc, st);
-        }
+        hipLaunchKernelGGL(opq_row_scale_kernel, dim3((unsigned)ceil_div(cn, 4)), dim3(256), 0, st, xc, cn, d, rs + c0);
+        int rc = check_launch("opq_row_scale");
+        if (rc) return rc;
+        // 256 x 256 tiles (512 threads, 160 KiB) wherever a row block spans at least one such
+        // tile; the 128 x 128 kernel for narrow matrices
+        rc = (d >= 256 && cn >= 256) ? launch_split<TileL, 4, 2, 2, 4>(xc, cn, d, rs + c0, bimg, hdr, yc, st)
+                                     : launch_split<TileS, 2, 2, 2, 2>(xc, cn, d, rs + c0, bimg, hdr, yc, st);
         if (rc) return rc;
     }
     return MIVQ_OK;

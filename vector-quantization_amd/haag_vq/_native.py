@@ -162,17 +162,14 @@ def _check(t: torch.Tensor, name: str, dtype: torch.dtype, ndim: Optional[int] =
 
 
 # ----------------------------------------------------------------- workspace
-_ws: dict = {}
-
-
 def workspace(nbytes: int, device: torch.device) -> torch.Tensor:
-    """Grow-only per-(device, stream) scratch buffer (the library never allocates)."""
-    key = (device.index, torch.cuda.current_stream(device).cuda_stream)
-    buf = _ws.get(key)
-    if buf is None or buf.numel() < nbytes:
-        buf = torch.empty(max(int(nbytes), 256), dtype=torch.uint8, device=device)
-        _ws[key] = buf
-    return buf
+    """Scratch buffer for one library call (the library never allocates).
+
+    Allocated per call from torch's caching allocator on the current stream: the block goes
+    back to that stream's pool when the caller drops it, and torch hands it out again only
+    to later work on the same stream, which is ordered after the kernels that used it.  No
+    module-level cache, so nothing outlives the call or follows a destroyed stream's handle."""
+    return torch.empty(max(int(nbytes), 256), dtype=torch.uint8, device=device)
 
 
 # ----------------------------------------------------------------- device info
@@ -273,9 +270,7 @@ def opq_rotate(x: torch.Tensor, A: torch.Tensor, transpose: bool = False,
 
 
 def opq_backend(d: Optional[int] = None) -> str:
-    """What the OPQ classes rotate with (for reports); d selects the kernel as opq.hip does."""
-    if d is not None and d % 32 == 0 and d >= 256:
-        return "opq_split_x_kernel + opq_glds_gemm_kernel: split-f16 MFMA GEMM (LDS-DMA staging), fp32 accuracy"
+    """What the OPQ classes rotate with (for reports)."""
     return "opq_row_scale_kernel + opq_split_gemm_kernel: split-f16 MFMA GEMM, fp32 accuracy"
 
 

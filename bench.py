@@ -146,14 +146,20 @@ def synth(n, d, seed, dev, kind="gaussian", centers_seed=12345, n_centers=4096, 
 
 
 def traffic_from_profile(workload: str):
-    """Per-launch HBM bytes from the committed rocprofv3 PMC summary, if it is for this workload."""
+    """Per-launch HBM bytes from the committed rocprofv3 PMC summary (profiles/traffic.json,
+    written by tools/traffic.py), if it is for this workload AND was measured on this build:
+    the entry's kernel-source hash must equal _native.kernel_source_hash() of the running tree
+    (a stale entry gives None, never a number from other kernels)."""
     p = ROOT / "profiles" / "traffic.json"
     if not p.exists():
         return None
     try:
-        return json.loads(p.read_text()).get(workload, {}).get("bytes_per_launch")
+        e = json.loads(p.read_text()).get(workload, {})
     except Exception:
         return None
+    if e.get("kernel_source_hash") != _native.kernel_source_hash():
+        return None
+    return e.get("bytes_per_launch")
 
 
 SETTLE = {"extra_steps": 0}
@@ -326,7 +332,7 @@ def adc_leg(X, C, codes, a, rank, world, dev, Q, k, gt_queries, reps=3, cpu=True
 
 
 # ------------------------------------------------------------------------- other configs
-def opq32_leg(a, dev, steps, warmup):
+def opq32_leg(a, dev, steps, warmup, cpu=True):
     from haag_vq.methods.optimized_product_quantization import OptimizedProductQuantizer
 
     d, M, n = 1536, 32, a.n
@@ -360,7 +366,9 @@ def opq32_leg(a, dev, steps, warmup):
     _, gi = _native.flat_search(Q[:100].contiguous(), X, 10)
     Xhat = opq.opq.rotate(_native.pq_decode(codes, C, 8), True)
     _, di = _native.flat_search(Q[:100].contiguous(), Xhat, 10)
-    del Xhat, X, Y
+    del Xhat
+    cpu_b = opq32_cpu_baseline(X, Y, codes, opq.opq.A_device, C, a.cpu_seconds / 2) if cpu else None
+    del X, Y
     g, r, dd = (t.cpu().numpy() for t in (gi, ai[:100], di))
     rec = lambda ref, x: float(np.mean([len(set(ref[j]) & set(x[j])) / 10 for j in range(len(ref))]))  # noqa: E731
     flops = 2.0 * d * d * n  # the fp32 GEMM's flops (algorithmic)
@@ -377,13 +385,41 @@ def opq32_leg(a, dev, steps, warmup):
                          "achieved": tfs, "peak": peak, "unit": "TFLOP/s (fp32-accurate)", "frac": tfs / peak,
                          "peak_note": "dense f16 MFMA peak / 3 (x_hi b_hi + x_hi b_lo + x_lo b_hi)" if split else
                                       "dense fp32 MFMA peak", "vs_fp32_mfma_peak": tfs / MFMA_F32_PEAK_TFS,
-                         "rotate_ms": rot_ms, "encode_call_ms": dev_ms - rot_ms},
+                         "rotate_ms": rot_ms, "encode_call_ms": dev_ms - rot_ms,
+                         "traffic": traffic_from_profile(f"opq32_rotate_{n}x{d}")},
             "adc": {"qps": a.nq / swall, "nq": a.nq, "k": 10, "recall@10": rec(g, r), "recall_queries": 100,
                     "recall@10_decode_exact": rec(g, dd), "topk_agreement_adc_vs_decode_exact": rec(dd, r),
-                    "ms_per_batch": swall * 1e3}}
+                    "ms_per_batch": swall * 1e3},
+            **({"cpu_baseline": cpu_b} if cpu_b else {})}
 
 
-def flatcodes_leg(a, dev, kind, steps, warmup):
+def opq32_cpu_baseline(X, Y, codes, A, C, target_s):
+    """OPQ encode on the host cores, as the reference's path runs it: the rotation x A^T as a BLAS
+    sgemm (numpy; faiss OPQMatrix.apply, optimized_product_quantization.py:30-31) followed by the
+    oracle's OpenMP PQ encode (faiss compute_codes), on a bounded sample of the same rows.
+    Checks: the oracle's encode of the GPU-rotated sample equals the GPU codes bit for bit; the
+    CPU-rotated sample's codes agree except at near-ties of the two roundings (fraction)."""
+    O = _oracle()
+    Ah, Cn = A.cpu().numpy(), C.cpu().numpy()
+    fn = lambda xs: O.pq_encode(np.ascontiguousarray(xs @ Ah.T), Cn)  # noqa: E731
+    n_cal = 1000
+    t0 = time.perf_counter()
+    fn(X[:n_cal].cpu().numpy())
+    dt = time.perf_counter() - t0
+    n_s = int(min(X.shape[0], max(n_cal, n_cal * target_s / max(dt, 1e-6))))
+    Xs = X[:n_s].cpu().numpy()
+    t0 = time.perf_counter()
+    ref_cpu = fn(Xs)
+    dt = time.perf_counter() - t0
+    got = codes[:n_s].cpu().numpy()
+    ref_gpu_rot = O.pq_encode(Y[:n_s].cpu().numpy(), Cn)
+    return {"value": n_s / dt, "unit": "vectors/s", "cores": O.cpu_threads(), "kind": "port",
+            "sample": f"first {n_s} rows: numpy sgemm rotation + oracle pq_encode (OpenMP), {dt:.1f} s wall",
+            "codes_equal_gpu_on_gpu_rotation": bool(np.array_equal(got, ref_gpu_rot)),
+            "code_agreement_cpu_rotation": float((got == ref_cpu).mean())}
+
+
+def flatcodes_leg(a, dev, kind, steps, warmup, cpu=True):
     d, n = 3072, a.n
     g = torch.Generator(device=dev)
     g.manual_seed(2)
@@ -393,7 +429,7 @@ def flatcodes_leg(a, dev, kind, steps, warmup):
         den = (hi - lo) + 1e-8
         enc = lambda: _native.sq_encode(X, lo, den, 8)  # noqa: E731
         dec = lambda c: _native.sq_decode(c, d, lo, den, 8)  # noqa: E731
-        bpv, kname = 4 * d + d, "sq_encode_f32_kernel"
+        bpv, kname = 4 * d + d, "sq_encode_f32_vec_kernel"
     else:
         enc = lambda: _native.rabitq_encode(X, None, _native.METRIC_L2)  # noqa: E731
         dec = lambda c: _native.rabitq_decode(c, d, None)  # noqa: E731
@@ -412,7 +448,8 @@ def flatcodes_leg(a, dev, kind, steps, warmup):
            "value": n / wall, "unit": "vectors/s", "ms_per_step": wall * 1e3, "dtype": "f32",
            "config": {"workload": f"{kind}_encode_{n}x{d}"},
            "roofline": {"bound": "hbm", "kernel": kname, "achieved": ach, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                        "frac": ach / HBM_PEAK_GBS, "bytes_per_vector": bpv, "kernel_ms": dev_ms},
+                        "frac": ach / HBM_PEAK_GBS, "bytes_per_vector": bpv, "kernel_ms": dev_ms,
+                        "traffic": traffic_from_profile(f"{kind}_encode_{n}x{d}")},
            "search": {"qps": 100 / swall, "nq": 100, "k": 10, "recall@10": rec(g_, r_),
                       "method": "decode + exact L2 scan of the reconstructions (the reference's flat search)"}}
     if kind == "rabitq1":  # RaBitQIndex: IndexRaBitQ estimator search (center = mean, qb = 4)
@@ -425,8 +462,45 @@ def flatcodes_leg(a, dev, kind, steps, warmup):
         out["estimator_search"] = {"qps": a.nq / ewall, "nq": a.nq, "k": 10, "qb": 4, "ms_per_batch": ewall * 1e3,
                                    "recall@10": rec(g_, ei[:100].cpu().numpy()),
                                    "method": "mivq_rabitq_search: int8 MFMA over sign bits + estimator + tiled top-k"}
+    if cpu:
+        out["cpu_baseline"] = flatcodes_cpu_baseline(kind, X, codes, lo if kind == "sq8" else None,
+                                                     den if kind == "sq8" else None, a.cpu_seconds / 2)
     del X
     return out
+
+
+def flatcodes_cpu_baseline(kind, X, codes, lo, den, target_s):
+    """The reference's CPU path for these encoders on a bounded sample of the same rows: SQ-8 as
+    ScalarQuantizer._compress_block writes it in numpy (scalar_quantization.py:52-68, one
+    thread), RaBitQ-1 as the oracle's OpenMP restatement of faiss RaBitQuantizer.compute_codes
+    (rabit_quantization.py:25-26); the sample's GPU codes must equal the CPU's."""
+    O = _oracle()
+    if kind == "sq8":
+        lo_h, den_h = lo.cpu().numpy(), den.cpu().numpy()
+        fn = lambda xs: O.sq_encode_numpy(xs, lo_h, den_h, 8)  # noqa: E731
+        cores, how = 1, "numpy restatement of ScalarQuantizer._compress_block (oracle.sq_encode_numpy)"
+    else:
+        fn = lambda xs: O.rabitq_encode(xs)  # noqa: E731
+        cores, how = O.cpu_threads(), "oracle/mivq_oracle.c rabitq_encode (OpenMP)"
+    n_cal = 2000
+    t0 = time.perf_counter()
+    fn(X[:n_cal].cpu().numpy())
+    dt = time.perf_counter() - t0
+    n_s = int(min(X.shape[0], max(n_cal, n_cal * target_s / max(dt, 1e-6))))
+    Xs = X[:n_s].cpu().numpy()
+    t0 = time.perf_counter()
+    ref = fn(Xs)
+    dt = time.perf_counter() - t0
+    got = codes[:n_s].cpu().numpy()
+    if kind == "sq8":
+        equal = bool(np.array_equal(got, ref))
+    else:  # sign bits exact, the two f32 factors within 1e-5 relative (faiss-internal order)
+        nb = (X.shape[1] + 7) // 8
+        f_g, f_r = got[:, nb:].copy().view(np.float32), ref[:, nb:].copy().view(np.float32)
+        equal = bool(np.array_equal(got[:, :nb], ref[:, :nb]) and
+                     np.all(np.abs(f_g - f_r) <= 1e-5 * np.maximum(np.abs(f_r), 1e-30)))
+    return {"value": n_s / dt, "unit": "vectors/s", "cores": cores, "kind": "port",
+            "sample": f"first {n_s} rows, {how}, {dt:.1f} s wall", "codes_equal_gpu": equal}
 
 
 def config5_leg(a, rank, world, dev, steps, warmup):
@@ -575,9 +649,10 @@ def main():
     configs = None
     if head_only and not a.no_configs:
         configs = {}
-        for name, fn in (("opq32", lambda: opq32_leg(a, dev, 3, 1)),
-                         ("sq8", lambda: flatcodes_leg(a, dev, "sq8", 5, 2)),
-                         ("rabitq1", lambda: flatcodes_leg(a, dev, "rabitq1", 5, 2))):
+        cb = not a.no_cpu_baseline
+        for name, fn in (("opq32", lambda: opq32_leg(a, dev, 3, 1, cpu=cb)),
+                         ("sq8", lambda: flatcodes_leg(a, dev, "sq8", 5, 2, cpu=cb)),
+                         ("rabitq1", lambda: flatcodes_leg(a, dev, "rabitq1", 5, 2, cpu=cb))):
             configs[name] = fn()
             torch.cuda.empty_cache()
             log(f"[rank 0] {name}: {configs[name]}")

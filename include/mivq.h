@@ -159,8 +159,8 @@ int mivq_rabitq_search(const uint8_t* codes, int64_t n, int32_t d, const float* 
 
 /* ------------------------------------------------------ Extended RaBitQ (B bits)
  * The element-wise / per-row steps of ExtendedRaBitQuantizer.compress / decompress
- * (extended_rabitq.py:125-199), fp64 like the reference; the two D x D rotations between
- * them (o . P and o_hat . P^T) are plain fp64 GEMMs issued by the host.
+ * (extended_rabitq.py:125-199), fp64 like the reference, and the two D x D rotations
+ * between them (o . P and o_hat . P^T, :140 and :196) as an fp64-MFMA GEMM.
  *   normalize : o = (x - c) / max(||x - c||, 1e-12), nrm = ||x - c||   (x f32 or f64)
  *   quantize  : s = s_raw * sqrt(D); idx = searchsorted(mid-levels, s); t = <s,s_hat>/<s_hat,s_hat>
  *               code row = MSB-first B-bit indices (ceil(D*B/8) bytes) ++ f32 nrm ++ f32 t
@@ -174,6 +174,9 @@ int mivq_extrabitq_dequantize(const uint8_t* codes, int64_t n, int32_t d, const 
                               int32_t nbits, double* o_hat, void* stream);
 int mivq_extrabitq_finish(const double* y, int64_t n, int32_t d, const uint8_t* codes,
                           int32_t nbits, const double* centroid, float* out, void* stream);
+/* s = o . P (transpose 0) or o . P^T (transpose 1); o, s: (n, d) f64 row-major, P: (d, d). */
+int mivq_extrabitq_rotate(const double* o, int64_t n, int32_t d, const double* P, int32_t transpose,
+                          double* s, void* stream);
 
 /* ------------------------------------------------------ ADC search
  * Flat asymmetric-distance search over PQ codes; the GPU counterpart of

@@ -214,6 +214,14 @@ def sq_encode(X: np.ndarray, lo: np.ndarray, den: np.ndarray, nbits: int) -> np.
     return out
 
 
+def sq_encode_numpy(X: np.ndarray, lo: np.ndarray, den: np.ndarray, nbits: int = 8) -> np.ndarray:
+    """ScalarQuantizer._compress_block (scalar_quantization.py:52-68) as the reference writes it,
+    in numpy (the CPU path the reference runs; 8 and 16 bits): ((X - lo) / den * (2^b - 1)),
+    rounded half to even, cast to uint8 / uint16.  The bench's CPU baseline for SQ-8."""
+    q = np.round((X - lo) / den * float((1 << nbits) - 1))
+    return q.astype(np.uint16 if nbits == 16 else np.uint8)
+
+
 def sq_decode(codes: np.ndarray, d: int, lo: np.ndarray, den: np.ndarray, nbits: int) -> np.ndarray:
     codes = np.ascontiguousarray(codes)
     n = codes.shape[0]

@@ -132,6 +132,24 @@ def test_extrabitq_kernels_match_reference_fixture(dev, golden_dir, nbits):
     np.testing.assert_allclose(rec, e[f"{tag}_recon"], rtol=1e-5, atol=1e-6)
 
 
+@pytest.mark.parametrize("n,d", [(1, 16), (77, 100), (300, 96), (257, 1536), (130, 3072)])
+@pytest.mark.parametrize("transpose", [False, True])
+def test_extrabitq_rotate_matches_fp64(dev, n, d, transpose):
+    """mivq_extrabitq_rotate (fp64 MFMA GEMM, extended_rabitq.py:140,196) against a numpy fp64
+    product: every element within a few ulps of sum |o_k P_kj| (fp64 accumulation, another
+    summation order), ragged n and d past the 128 x 128 tiles and 16-wide K slices."""
+    from haag_vq import _native
+
+    rng = np.random.default_rng(n * 7 + d)
+    o = rng.standard_normal((n, d))
+    P, _ = np.linalg.qr(rng.standard_normal((d, d)))
+    got = _h(_native.extrabitq_rotate(_t(o, dev), _t(P, dev), transpose))
+    Pm = P.T if transpose else P
+    ref = o @ Pm
+    scale = np.abs(o) @ np.abs(Pm)
+    assert np.all(np.abs(got - ref) <= 1e-14 * d * scale + 1e-300), float(np.max(np.abs(got - ref) / scale))
+
+
 def _prep_offsets(M, dsub, ksub=256):
     """Byte offsets inside the mivq_pq_prepare buffer (mirror of PqPrepLayout, mivq_common.h)."""
     al = lambda v: (v + 255) // 256 * 256  # noqa: E731

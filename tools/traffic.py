@@ -1,8 +1,11 @@
-"""Write profiles/traffic.json: HBM bytes per mivq_pq_encode call from a tools/pmc.sh run.
+"""Write profiles/traffic.json: HBM bytes per launch of each benched kernel group, from a
+tools/pmc_traffic.sh run, stamped with the kernel-source hash of the tree that was profiled
+(bench.py refuses an entry whose hash differs from the running tree's).
 
-usage: python tools/traffic.py gpurun_out/pmc_<tag> <workload> [last_n]
-Sums the per-launch HBM bytes (FETCH_SIZE x2 + WRITE_SIZE, gfx950 corrections as in
-tools/pmc_summary.py) of the four kernels of one encode call.
+usage: python tools/traffic.py gpurun_out/pmc_traffic [last_n]
+Per dispatch: FETCH_SIZE x 2 (gfx950: FETCH_SIZE counts half the bytes of a wide coalesced
+read, MI355X_MICROARCH.md HBM section) + WRITE_SIZE, both in KiB; the mean over the last_n
+dispatches of each kernel, summed over the kernels of a workload.
 """
 import csv
 import glob
@@ -11,32 +14,51 @@ import sys
 from collections import defaultdict
 from pathlib import Path
 
-KERNELS = ("pq_encode_cs_kernel", "pq_resolve_merged", "pq_transpose_codes")
+ROOT = Path(__file__).resolve().parent.parent
+sys.path.insert(0, str(ROOT / "vector-quantization_amd"))
+
+# workload -> kernel-name substrings (template arguments select the shape)
+WORKLOADS = {
+    "pq16_encode_1000000x1536_gaussian": ["pq_encode_cs_kernelILi6ELi3ELi0ELi96", "pq_resolve_merged_kernelILi6ELi96",
+                                          "pq_transpose_codes16_kernelILi16"],
+    "opq32_rotate_1000000x1536": ["opq_row_scale_kernel", "opq_split_gemm_kernel"],
+    "sq8_encode_1000000x3072": ["sq_encode_f32_vec_kernel"],
+    "rabitq1_encode_1000000x3072": ["rabitq_encode_kernelILb0"],
+}
 
 
 def per_launch(root, sub, last_n):
     vals = defaultdict(list)
-    for f in sorted(glob.glob(f"{root}/p*/run_counter_collection.csv")):
+    for f in sorted(glob.glob(f"{root}/p*/**/*counter_collection.csv", recursive=True)):
         rows = [r for r in csv.DictReader(open(f)) if sub in r["Kernel_Name"]]
         ids = sorted({int(r["Dispatch_Id"]) for r in rows})[-last_n:]
         for r in rows:
             if int(r["Dispatch_Id"]) in ids and r["Counter_Name"] in ("FETCH_SIZE", "WRITE_SIZE"):
                 vals[r["Counter_Name"]].append(float(r["Counter_Value"]))
-    fetch = sum(vals["FETCH_SIZE"]) / max(1, len(vals["FETCH_SIZE"]))
+    if not vals["FETCH_SIZE"]:
+        return None
+    fetch = sum(vals["FETCH_SIZE"]) / len(vals["FETCH_SIZE"])
     write = sum(vals["WRITE_SIZE"]) / max(1, len(vals["WRITE_SIZE"]))
     return fetch * 1024 * 2 + write * 1024
 
 
 def main():
-    root, workload = sys.argv[1], sys.argv[2]
-    last_n = int(sys.argv[3]) if len(sys.argv) > 3 else 4
-    parts = {k: per_launch(root, k, last_n) for k in KERNELS}
-    out_path = Path(__file__).resolve().parent.parent / "profiles" / "traffic.json"
-    data = json.loads(out_path.read_text()) if out_path.exists() else {}
-    data[workload] = {"bytes_per_launch": sum(parts.values()), "per_kernel": parts,
-                      "source": f"{root} (rocprofv3 --pmc FETCH_SIZE/WRITE_SIZE, FETCH x2 gfx950 correction, KiB)"}
+    from haag_vq import _native
+
+    root = sys.argv[1]
+    last_n = int(sys.argv[2]) if len(sys.argv) > 2 else 3
+    out_path = ROOT / "profiles" / "traffic.json"
+    data = {}
+    for w, kernels in WORKLOADS.items():
+        parts = {k: per_launch(root, k, last_n) for k in kernels}
+        if all(v is None for v in parts.values()):
+            continue
+        data[w] = {"bytes_per_launch": sum(v for v in parts.values() if v), "per_kernel": parts,
+                   "kernel_source_hash": _native.kernel_source_hash(),
+                   "source": f"{root}: rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE (separate passes), FETCH x2 "
+                             f"(gfx950 correction), mean of the last {last_n} dispatches per kernel"}
     out_path.write_text(json.dumps(data, indent=1) + "\n")
-    print(json.dumps(data[workload], indent=1))
+    print(json.dumps(data, indent=1))
 
 
 if __name__ == "__main__":

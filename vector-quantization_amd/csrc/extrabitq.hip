@@ -3,12 +3,15 @@
 // Restates ExtendedRaBitQuantizer.compress / decompress
 // (/root/reference/src/haag_vq/methods/extended_rabitq.py:125-199), all in fp64 like numpy:
 //   encode: r = x - c; nrm = ||r||; o = r / max(nrm, 1e-12)                 [normalize]
-//           s = (o . P) * sqrt(D)   (the D x D product is a plain fp64 GEMM on the host side)
+//           s = (o . P) * sqrt(D)   (the D x D product: erq_rotate_kernel, fp64 MFMA)
 //           idx = searchsorted(mid-levels, s) (left); s_hat = levels[idx]
 //           t = <s, s_hat> / <s_hat, s_hat>  (1 when the denominator <= 1e-12)
 //           row = B-bit idx packed MSB-first (np.packbits) ++ f32 nrm ++ f32 t   [quantize]
 //   decode: o_hat = (levels[idx] / sqrt(D)) * t                              [dequantize]
 //           x_hat = f32((o_hat . P^T) * nrm + c)                             [finish]
+// The two D x D rotations (o . P, o_hat . P^T; extended_rabitq.py:140,196) run on
+// erq_rotate_kernel: v_mfma_f64_16x16x4_f64, 128 x 128 output tiles, K slices of 16 staged
+// through LDS (double-buffered), fp64 accumulation (mivq_extrabitq_rotate).
 // One wavefront per row for the reductions (tree order: the factors match numpy to ~1e-15
 // relative, the indices are exact except where s lies within rounding of a level midpoint).
 #include "mivq_common.h"
@@ -130,6 +133,108 @@ __global__ void erq_finish_kernel(const double* __restrict__ y, int64_t n, int d
     out[e] = (float)__dadd_rn(__dmul_rn(y[e], nr), c[j]);
 }
 
+
+// ---------------------------------------------------------------- fp64 rotation GEMM
+// s = o . op(P) for the (n, d) row block o and the (d, d) matrix P: op(P) = P (transpose 0,
+// encode: extended_rabitq.py:140) or P^T (transpose 1, decode: :196).  Workgroup: 256 threads,
+// a 128 x 128 tile of s (4 waves of 64 x 64 = 4 x 4 blocks of v_mfma_f64_16x16x4_f64, 16
+// accumulators of 4 doubles per lane), K in slices of 16 through two LDS stages.  Operand maps
+// (cdna_hip_programming.md, f64 MFMA): A: lane l holds A[l & 15][l >> 4], B: B[l >> 4][l & 15],
+// D: col = l & 15, row = (l >> 4) + 4 reg.  Every product is exact fp64 FMA accumulation
+// (sum order: the MFMA's over k, slices ascending); rows past n / columns past d are masked.
+constexpr int kRotT = 128, kRotK = 16;
+constexpr int kRotAP = kRotK + 1;   // A stage row pitch (doubles): [row][k]
+constexpr int kRotBP = kRotT + 1;   // B stage row pitch (doubles): [k][col]
+typedef double f64x4 __attribute__((ext_vector_type(4)));
+
+__global__ __launch_bounds__(256) void erq_rotate_kernel(const double* __restrict__ o, int64_t n, int d,
+                                                         const double* __restrict__ P, int transpose,
+                                                         double* __restrict__ s, int64_t ctiles) {
+    __shared__ double As[2][kRotT * kRotAP];
+    __shared__ double Bs[2][kRotK * kRotBP];
+    const int tid = threadIdx.x, l = tid & 63, w = tid >> 6;
+    const int64_t r0 = (int64_t)(blockIdx.x / ctiles) * kRotT;
+    const int c0 = (int)(blockIdx.x % ctiles) * kRotT;
+    const int wr = w >> 1, wc = w & 1;  // wave tile: rows wr*64.., cols wc*64..
+    f64x4 acc[4][4];
+#pragma unroll
+    for (int a = 0; a < 4; ++a)
+#pragma unroll
+        for (int b = 0; b < 4; ++b) acc[a][b] = (f64x4){0.0, 0.0, 0.0, 0.0};
+
+    // staging: A slice = 128 rows x 16 k (each thread 8 doubles: row tid / 2, k 8 (tid & 1) ..);
+    // B slice = 16 k x 128 cols (each thread 8 doubles)
+    double ra[8], rb[8];
+    auto gload = [&](int k0) __attribute__((always_inline)) {
+        {
+            const int rr = tid >> 1, kk = 8 * (tid & 1);
+            const int64_t gr = r0 + rr;
+#pragma unroll
+            for (int u = 0; u < 8; ++u)
+                ra[u] = (gr < n && k0 + kk + u < d) ? o[gr * d + k0 + kk + u] : 0.0;
+        }
+        if (transpose == 0) {  // B[k][j] = P[k][j]: rows of P, 8 consecutive columns per thread
+            const int kk = tid >> 4, jj = 8 * (tid & 15);
+#pragma unroll
+            for (int u = 0; u < 8; ++u)
+                rb[u] = (k0 + kk < d && c0 + jj + u < d) ? P[(int64_t)(k0 + kk) * d + c0 + jj + u] : 0.0;
+        } else {  // B[k][j] = P[j][k]: column j of op(P) is row j of P, 8 consecutive k per thread
+            const int jj = tid >> 1, kk = 8 * (tid & 1);
+#pragma unroll
+            for (int u = 0; u < 8; ++u)
+                rb[u] = (c0 + jj < d && k0 + kk + u < d) ? P[(int64_t)(c0 + jj) * d + k0 + kk + u] : 0.0;
+        }
+    };
+    auto sstore = [&](int st) __attribute__((always_inline)) {
+        {
+            const int rr = tid >> 1, kk = 8 * (tid & 1);
+#pragma unroll
+            for (int u = 0; u < 8; ++u) As[st][rr * kRotAP + kk + u] = ra[u];
+        }
+        if (transpose == 0) {
+            const int kk = tid >> 4, jj = 8 * (tid & 15);
+#pragma unroll
+            for (int u = 0; u < 8; ++u) Bs[st][kk * kRotBP + jj + u] = rb[u];
+        } else {
+            const int jj = tid >> 1, kk = 8 * (tid & 1);
+#pragma unroll
+            for (int u = 0; u < 8; ++u) Bs[st][(kk + u) * kRotBP + jj] = rb[u];
+        }
+    };
+    const int nk = (d + kRotK - 1) / kRotK;
+    gload(0);
+    sstore(0);
+    __syncthreads();
+    const int fi = l & 15, fk = l >> 4;
+    for (int ks = 0; ks < nk; ++ks) {
+        const int st = ks & 1;
+        if (ks + 1 < nk) gload((ks + 1) * kRotK);
+#pragma unroll
+        for (int k4 = 0; k4 < kRotK; k4 += 4) {
+            double af[4], bf[4];
+#pragma unroll
+            for (int a = 0; a < 4; ++a) af[a] = As[st][(wr * 64 + a * 16 + fi) * kRotAP + k4 + fk];
+#pragma unroll
+            for (int b = 0; b < 4; ++b) bf[b] = Bs[st][(k4 + fk) * kRotBP + wc * 64 + b * 16 + fi];
+#pragma unroll
+            for (int a = 0; a < 4; ++a)
+#pragma unroll
+                for (int b = 0; b < 4; ++b) acc[a][b] = __builtin_amdgcn_mfma_f64_16x16x4f64(af[a], bf[b], acc[a][b], 0, 0, 0);
+        }
+        if (ks + 1 < nk) sstore(st ^ 1);
+        __syncthreads();
+    }
+#pragma unroll
+    for (int a = 0; a < 4; ++a)
+#pragma unroll
+        for (int b = 0; b < 4; ++b)
+#pragma unroll
+            for (int g = 0; g < 4; ++g) {
+                const int64_t row = r0 + wr * 64 + a * 16 + fk + 4 * g;
+                const int col = c0 + wc * 64 + b * 16 + fi;
+                if (row < n && col < d) s[row * d + col] = acc[a][b][g];
+            }
+}
 }  // namespace
 }  // namespace mivq
 
@@ -177,4 +282,17 @@ extern "C" int mivq_extrabitq_finish(const double* y, int64_t n, int32_t d, cons
     hipLaunchKernelGGL(erq_finish_kernel, dim3((unsigned)ceil_div(n * (int64_t)d, 256)), dim3(256), 0,
                        as_stream(stream), y, n, d, codes, nbits, centroid, out);
     return check_launch("extrabitq_finish");
+}
+
+extern "C" int mivq_extrabitq_rotate(const double* o, int64_t n, int32_t d, const double* P, int32_t transpose,
+                                     double* s, void* stream) {
+    MIVQ_REQUIRE(n >= 0 && d > 0, MIVQ_ERR_INVALID, "extrabitq_rotate: bad sizes n=%lld d=%d", (long long)n, d);
+    MIVQ_REQUIRE(transpose == 0 || transpose == 1, MIVQ_ERR_INVALID, "extrabitq_rotate: transpose must be 0 or 1");
+    if (n == 0) return MIVQ_OK;
+    MIVQ_REQUIRE(o && P && s && o != s, MIVQ_ERR_INVALID, "extrabitq_rotate: null or aliased pointer");
+    const int64_t ct = ceil_div(d, kRotT), tiles = ceil_div(n, kRotT) * ct;
+    MIVQ_REQUIRE(tiles < ((int64_t)1 << 31), MIVQ_ERR_UNSUPPORTED, "extrabitq_rotate: n=%lld too large", (long long)n);
+    hipLaunchKernelGGL(erq_rotate_kernel, dim3((unsigned)tiles), dim3(256), 0, as_stream(stream), o, n, d, P, transpose, s,
+                       ct);
+    return check_launch("extrabitq_rotate");
 }

@@ -70,6 +70,7 @@ SIGNATURES = {
     "mivq_extrabitq_quantize": (_c.c_int, [_vp, _i64, _i32, _vp, _i32, _vp, _vp, _vp]),
     "mivq_extrabitq_dequantize": (_c.c_int, [_vp, _i64, _i32, _vp, _i32, _vp, _vp]),
     "mivq_extrabitq_finish": (_c.c_int, [_vp, _i64, _i32, _vp, _i32, _vp, _vp, _vp]),
+    "mivq_extrabitq_rotate": (_c.c_int, [_vp, _i64, _i32, _vp, _i32, _vp, _vp]),
     "mivq_adc_lut": (_c.c_int, [_vp, _i64, _i32, _i32, _i32, _vp, _i32, _vp, _vp]),
     "mivq_adc_search_workspace_bytes": (_sz, [_i64, _i64, _i32, _i32, _i32]),
     "mivq_adc_search": (_c.c_int, [_vp, _i64, _vp, _i64, _i32, _i32, _i32, _i64, _vp, _sz, _vp, _vp, _vp]),
@@ -162,6 +163,20 @@ def _check(t: torch.Tensor, name: str, dtype: torch.dtype, ndim: Optional[int] =
 
 
 # ----------------------------------------------------------------- workspace
+def kernel_source_hash() -> str:
+    """sha256 (first 16 hex digits) of the library's sources (csrc/*.hip, csrc/*.h,
+    include/mivq.h, in name order): stamps PMC-derived numbers with the build they describe."""
+    import hashlib
+
+    h = hashlib.sha256()
+    csrc = _PKG_ROOT / "csrc"
+    files = sorted(list(csrc.glob("*.hip")) + list(csrc.glob("*.h"))) + [_PKG_ROOT.parent / "include" / "mivq.h"]
+    for f in files:
+        h.update(f.name.encode())
+        h.update(f.read_bytes())
+    return h.hexdigest()[:16]
+
+
 def workspace(nbytes: int, device: torch.device) -> torch.Tensor:
     """Scratch buffer for one library call (the library never allocates).
 
@@ -400,9 +415,21 @@ def extrabitq_code_size(d: int, nbits: int) -> int:
     return (d * nbits + 7) // 8 + 8
 
 
+def extrabitq_rotate(o: torch.Tensor, P: torch.Tensor, transpose: bool) -> torch.Tensor:
+    """o . P (or o . P^T) in fp64 on the library's MFMA GEMM (extended_rabitq.py:140,196)."""
+    _check(o, "o", torch.float64, 2)
+    _check(P, "P", torch.float64, 2)
+    n, d = o.shape
+    if tuple(P.shape) != (d, d):
+        raise ValueError(f"P shape {tuple(P.shape)} != {(d, d)}")
+    out = torch.empty((n, d), dtype=torch.float64, device=o.device)
+    _call("mivq_extrabitq_rotate", _ptr(o), n, d, _ptr(P), 1 if transpose else 0, _ptr(out), _stream())
+    return out
+
+
 def extrabitq_encode(x: torch.Tensor, c: torch.Tensor, P: torch.Tensor, levels: torch.Tensor,
                      nbits: int) -> torch.Tensor:
-    """Codes of ExtendedRaBitQuantizer.compress; the o . P rotation is an fp64 library GEMM."""
+    """Codes of ExtendedRaBitQuantizer.compress (the o . P rotation on mivq_extrabitq_rotate)."""
     if x.dtype not in (torch.float32, torch.float64):
         raise ValueError(f"extrabitq: unsupported dtype {x.dtype}")
     _check(x, "x", x.dtype, 2)
@@ -414,7 +441,7 @@ def extrabitq_encode(x: torch.Tensor, c: torch.Tensor, P: torch.Tensor, levels: 
     nrm = torch.empty((n,), dtype=torch.float64, device=x.device)
     _call("mivq_extrabitq_normalize", _ptr(x), 1 if x.dtype == torch.float64 else 0, n, d, _ptr(c), _ptr(o),
           _ptr(nrm), _stream())
-    s_raw = (o @ P).contiguous()
+    s_raw = extrabitq_rotate(o, P, False)
     codes = torch.empty((n, extrabitq_code_size(d, nbits)), dtype=torch.uint8, device=x.device)
     _call("mivq_extrabitq_quantize", _ptr(s_raw), n, d, _ptr(levels), nbits, _ptr(nrm), _ptr(codes), _stream())
     return codes
@@ -429,7 +456,7 @@ def extrabitq_decode(codes: torch.Tensor, c: torch.Tensor, P: torch.Tensor, leve
         raise ValueError(f"codes have {codes.shape[1]} bytes per row, expected {extrabitq_code_size(d, nbits)}")
     o_hat = torch.empty((n, d), dtype=torch.float64, device=codes.device)
     _call("mivq_extrabitq_dequantize", _ptr(codes), n, d, _ptr(levels), nbits, _ptr(o_hat), _stream())
-    y = (o_hat @ P.T).contiguous()
+    y = extrabitq_rotate(o_hat, P, True)
     out = torch.empty((n, d), dtype=torch.float32, device=codes.device)
     _call("mivq_extrabitq_finish", _ptr(y), n, d, _ptr(codes), nbits, _ptr(c), _ptr(out), _stream())
     return out

@@ -45,6 +45,7 @@ extern "C" {
 #define MIVQ_PQ_AUTO 0u        /* fp16-MFMA candidate filter + exact fp32 re-check when supported */
 #define MIVQ_PQ_FORCE_EXACT 1u /* exact fp32 VALU scan of every centroid (canonical order)     */
 #define MIVQ_PQ_LEGACY_MFMA 2u /* diagnostic: subspace-looping MFMA kernel + separate resolve */
+#define MIVQ_PQ_LEGACY_EXACT 4u /* diagnostic: lane-per-row exact kernel instead of the tiled one */
 
 /* Metric enum values follow faiss / haag_vq.utils.faiss_utils.MetricType (faiss_utils.py:3-5). */
 #define MIVQ_METRIC_INNER_PRODUCT 0

@@ -38,6 +38,8 @@ PQ_SHAPES = [
     (300, 1024, 8, 8),      # wide filter KS=8 (dsub 128, 4 waves, codebook read from L2)
     (300, 1536, 8, 8),      # wide filter KS=12 (dsub 192: config #1's PQ8 at D=1536)
     (300, 1120, 8, 8),      # wide filter KS=9 (dsub 140, padded K)
+    (200, 1024, 4, 8),      # dsub 256 (M = 4 at D = 1024: the sweep's `--pq-subquantizers 4`)
+    (150, 1536, 4, 8),      # dsub 384 (M = 4 at D = 1536)
     (200, 48, 6, 8),        # dsub 8, KS=1
     (257, 48, 12, 8),       # dsub 4
     (256, 16, 4, 4),        # nbits 4 (faiss bit stream)
@@ -70,6 +72,9 @@ def test_pq_encode_bit_exact(dev, oracle, n, d, M, nbits):
     np.testing.assert_array_equal(got_exact, ref)
     got_legacy = _h(_native.pq_encode(_t(X, dev), Cd, prep, nbits, flags_extra=_native.MIVQ_PQ_LEGACY_MFMA))
     np.testing.assert_array_equal(got_legacy, ref)
+    got_lexact = _h(_native.pq_encode(_t(X, dev), Cd, prep, nbits, exact=True,
+                                      flags_extra=_native.MIVQ_PQ_LEGACY_EXACT))
+    np.testing.assert_array_equal(got_lexact, ref)
 
 
 @pytest.mark.parametrize("kind", ["gaussian", "clustered", "duplicates"])
@@ -94,6 +99,8 @@ def test_pq_encode_bit_exact_trained_codebooks(dev, oracle, kind):
     prep = _native.pq_prepare(C, 8)
     np.testing.assert_array_equal(_h(_native.pq_encode(Xd, C, prep, 8)), ref)
     np.testing.assert_array_equal(_h(_native.pq_encode(Xd, C, prep, 8, flags_extra=_native.MIVQ_PQ_LEGACY_MFMA)), ref)
+    # the tiled exact kernel (register-blocked VALU GEMM, cross-lane argmin) on the same near-ties
+    np.testing.assert_array_equal(_h(_native.pq_encode(Xd, C, prep, 8, exact=True)), ref)
 
 
 def test_pq_encode_bit_exact_config5_shape(dev, oracle):
@@ -442,11 +449,13 @@ def test_opq_rotate(dev):
         assert np.all(np.abs(back - ref2) <= tol + 1e-30)
 
 
-def test_kmeans_update_deterministic(dev):
+@pytest.mark.parametrize("n,M,ksub,dsub", [(5000, 4, 16, 8), (600, 2, 8, 384), (300, 1, 4, 1536)])
+def test_kmeans_update_deterministic(dev, n, M, ksub, dsub):
+    """Centroid update: ascending-row sums, empty clusters keep their value; dsub past 256
+    (M = 4 at D = 1536 is dsub 384, the reference sweep's `--pq-subquantizers 4`)."""
     from haag_vq import _native
 
     rng = np.random.default_rng(8)
-    n, M, ksub, dsub = 5000, 4, 16, 8
     X = rng.standard_normal((n, M * dsub)).astype(np.float32)
     assign = rng.integers(0, ksub - 1, size=(n, M)).astype(np.uint8)  # last cluster empty
     C0 = rng.standard_normal((M, ksub, dsub)).astype(np.float32)

@@ -93,14 +93,17 @@ def test_pq_d_not_divisible_raises_assertion():
 
 # ----------------------------------------------------------------- PQ / OPQ classes
 
-def test_pq_class_codes_equal_oracle(oracle):
+@pytest.mark.parametrize("n,d,M", [(3000, 64, 8), (1200, 1536, 4)])
+def test_pq_class_codes_equal_oracle(oracle, n, d, M):
+    """fit / compress / decompress through the class; M = 4 at D = 1536 (dsub 384) is the
+    reference sweep's `--pq-subquantizers 4` on dbpedia (sweep.py:89)."""
     from haag_vq.methods.product_quantization import ProductQuantizer
 
-    X = _data(n=3000, d=64)
-    pq = ProductQuantizer(M=8, B=8)
+    X = _data(n=n, d=d)
+    pq = ProductQuantizer(M=M, B=8)
     pq.fit(X)
     codes = pq.compress(X)
-    assert codes.shape == (3000, 8) and codes.dtype == np.uint8
+    assert codes.shape == (n, M) and codes.dtype == np.uint8
     C = np.stack(pq.codebooks).astype(np.float32)
     np.testing.assert_array_equal(codes, oracle.pq_encode(X, C))
     np.testing.assert_array_equal(pq.decompress(codes), oracle.pq_decode(codes, C))

@@ -249,6 +249,109 @@ __global__ __launch_bounds__(64) void pq_encode_exact_kernel(
     if (row < n) out[row * M + m] = (uint8_t)bi;
 }
 
+// ------------------------------------------------------------------ tiled exact encode
+// The exact path for subspaces the MFMA filter does not take (dsub > 192, or a forced exact
+// assignment), ksub = 256, dsub % 4 == 0.  A VALU register-blocked GEMM: grid
+// (ceil(n/128), M), block 256; thread (rg = tid >> 4, cg = tid & 15) owns rows rg*8 .. +8
+// and centroids {64 q + 4 cg + i : q, i < 4}, 128 fp32 accumulators as packed pairs
+// (v_pk_fma_f32).  Each accumulator is still ONE fma chain over t = 0, 1, ..., dsub-1 from
+// 0.0f, then s = fma(-2, acc, cn[k]) -- the canonical score, so codes are bit-exact.  dsub is
+// walked in chunks of kXT dims: x chunk transposed to xs[t][row] (rows as b128 broadcasts),
+// codebook chunk cs[t][k] from the transposed codebook ct (conflict-free b128 reads).
+// Argmin: lexicographic (score, k) within the thread, then across the 16 cg lanes by xor
+// shuffles -- the same winner as a strict-< scan in ascending k (NaN never wins, ties go to
+// the lower index, all non-finite-or-+inf rows give 0).
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+constexpr int kXT = 32;          // dims per chunk
+constexpr int kXRows = 128;      // rows per block
+constexpr int kXsStride = kXRows + 4;
+__global__ __launch_bounds__(256, 2) void pq_encode_exact_tiled_kernel(
+    const float* __restrict__ x, int64_t n, int d, int M, int dsub, const float* __restrict__ ct,
+    const float* __restrict__ cn, uint8_t* __restrict__ out) {
+    __shared__ __attribute__((aligned(16))) float xs[kXT * kXsStride];
+    __shared__ __attribute__((aligned(16))) float cs[kXT * 256];
+    const int tid = threadIdx.x;
+    const int rg = tid >> 4, cg = tid & 15;
+    const int m = blockIdx.y;
+    const int64_t r0 = (int64_t)blockIdx.x * kXRows;
+    const float* ctm = ct + (int64_t)m * dsub * 256;
+    f32x2 acc[8][8];
+#pragma unroll
+    for (int r = 0; r < 8; ++r)
+#pragma unroll
+        for (int j = 0; j < 8; ++j) acc[r][j] = f32x2{0.0f, 0.0f};
+    for (int t0 = 0; t0 < dsub; t0 += kXT) {
+        const int tl = min(kXT, dsub - t0);  // multiple of 4
+        __syncthreads();
+        // x chunk: 128 rows x tl dims, float4 per thread-step (8 lanes per row segment)
+        for (int e = tid; e < kXRows * (kXT / 4); e += 256) {
+            const int rr = e >> 3, tq = e & 7;
+            const int64_t row = r0 + rr;
+            float4 v = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+            if (row < n && tq * 4 < tl)
+                v = *reinterpret_cast<const float4*>(x + row * d + (int64_t)m * dsub + t0 + tq * 4);
+            xs[(tq * 4 + 0) * kXsStride + rr] = v.x;
+            xs[(tq * 4 + 1) * kXsStride + rr] = v.y;
+            xs[(tq * 4 + 2) * kXsStride + rr] = v.z;
+            xs[(tq * 4 + 3) * kXsStride + rr] = v.w;
+        }
+        for (int e = tid; e < tl * 64; e += 256) {
+            const int tt = e >> 6, kq = e & 63;
+            *reinterpret_cast<float4*>(cs + tt * 256 + kq * 4) =
+                *reinterpret_cast<const float4*>(ctm + (int64_t)(t0 + tt) * 256 + kq * 4);
+        }
+        __syncthreads();
+#pragma unroll 2
+        for (int t = 0; t < tl; ++t) {
+            const float4 xa = *reinterpret_cast<const float4*>(xs + t * kXsStride + rg * 8);
+            const float4 xb = *reinterpret_cast<const float4*>(xs + t * kXsStride + rg * 8 + 4);
+            const float xv[8] = {xa.x, xa.y, xa.z, xa.w, xb.x, xb.y, xb.z, xb.w};
+            f32x2 c2[8];
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                const float4 c = *reinterpret_cast<const float4*>(cs + t * 256 + q * 64 + cg * 4);
+                c2[2 * q] = f32x2{c.x, c.y};
+                c2[2 * q + 1] = f32x2{c.z, c.w};
+            }
+#pragma unroll
+            for (int r = 0; r < 8; ++r) {
+                const f32x2 xx = f32x2{xv[r], xv[r]};
+#pragma unroll
+                for (int j = 0; j < 8; ++j) acc[r][j] = __builtin_elementwise_fma(xx, c2[j], acc[r][j]);
+            }
+        }
+    }
+    const float* cnm = cn + (int64_t)m * 256;
+    float cnv[16];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+        const float4 c = *reinterpret_cast<const float4*>(cnm + q * 64 + cg * 4);
+        cnv[4 * q] = c.x; cnv[4 * q + 1] = c.y; cnv[4 * q + 2] = c.z; cnv[4 * q + 3] = c.w;
+    }
+    int mine = 0;  // the code of row rg*8 + cg (cg < 8)
+#pragma unroll
+    for (int r = 0; r < 8; ++r) {
+        float best = INFINITY;
+        int bi = 0;
+#pragma unroll
+        for (int j = 0; j < 16; ++j) {
+            const float a = (j & 1) ? acc[r][j >> 1].y : acc[r][j >> 1].x;
+            const float s = __builtin_fmaf(-2.0f, a, cnv[j]);
+            const int k = (j >> 2) * 64 + cg * 4 + (j & 3);
+            if (s < best) { best = s; bi = k; }  // k ascends within the thread
+        }
+#pragma unroll
+        for (int off = 1; off < 16; off <<= 1) {
+            const float ob = __shfl_xor(best, off, 16);
+            const int oi = __shfl_xor(bi, off, 16);
+            if (ob < best || (ob == best && oi < bi)) { best = ob; bi = oi; }
+        }
+        if (cg == r) mine = bi;
+    }
+    const int64_t row = r0 + rg * 8 + cg;
+    if (cg < 8 && row < n) out[row * M + m] = (uint8_t)mine;
+}
+
 // ------------------------------------------------------------------------- MFMA encode
 // Error window (all in accumulator units, i.e. scaled by sigma*tau; a_k = <x,c_k> - |c_k|^2/2
 // is maximised, Xs >= sigma*||x_m||, Cs = tau*max_k ||c_k||, x~ = f16(sigma x), c~_k = f16(tau c_k),
@@ -585,13 +688,17 @@ __global__ void pq_decode_kernel(const uint8_t* __restrict__ codes, int64_t n, i
 // ------------------------------------------------------------------- k-means update
 // grid (ksub, M), block 256: block (k, m) gathers, in ascending row order, the rows assigned
 // to centroid k of subspace m and sums their subvectors sequentially (deterministic).
+constexpr int kKmDims = 8;  // dims per thread of kmeans_update_kernel: dsub <= 2048
+
 __global__ __launch_bounds__(256) void kmeans_update_kernel(
     const float* __restrict__ x, int64_t n, int d, int M, int ksub, int dsub,
     const uint8_t* __restrict__ assign, float* __restrict__ centroids, int32_t* __restrict__ counts) {
     __shared__ int64_t rows[256];
     __shared__ int nsel;
     const int k = blockIdx.x, m = blockIdx.y, tid = threadIdx.x;
-    float sum = 0.0f;  // thread tid owns dimension tid (dsub <= 256)
+    float sum[kKmDims];  // thread tid owns dimensions tid + 256 u (dsub <= 256 kKmDims)
+#pragma unroll
+    for (int u = 0; u < kKmDims; ++u) sum[u] = 0.0f;
     int64_t count = 0;
     for (int64_t base = 0; base < n; base += 256) {
         const int64_t rr = base + tid;
@@ -611,13 +718,17 @@ __global__ __launch_bounds__(256) void kmeans_update_kernel(
         if (hit) rows[wave_off[wv] + __popcll(b & ((1ull << ln) - 1ull))] = rr;
         __syncthreads();
         const int ns = nsel;
-        if (tid < dsub)
-            for (int q = 0; q < ns; ++q) sum += x[rows[q] * d + (int64_t)m * dsub + tid];
+#pragma unroll
+        for (int u = 0; u < kKmDims; ++u)
+            if (tid + 256 * u < dsub)
+                for (int q = 0; q < ns; ++q) sum[u] += x[rows[q] * d + (int64_t)m * dsub + tid + 256 * u];
         count += ns;
         __syncthreads();
     }
-    if (tid < dsub && count > 0)
-        centroids[((int64_t)m * ksub + k) * dsub + tid] = sum / (float)count;
+#pragma unroll
+    for (int u = 0; u < kKmDims; ++u)
+        if (tid + 256 * u < dsub && count > 0)
+            centroids[((int64_t)m * ksub + k) * dsub + tid + 256 * u] = sum[u] / (float)count;
     if (tid == 0) counts[(int64_t)m * ksub + k] = (int32_t)count;
 }
 
@@ -759,6 +870,11 @@ extern "C" int mivq_pq_encode(const float* x, int64_t n, int32_t d, int32_t M, i
                            x, n, d, M, L.dsub, ct, cn, fl, nwords, u8);
         int rc = check_launch("pq_resolve");
         if (rc) return rc;
+    } else if (L.ksub == 256 && L.dsub % 4 == 0 && aligned && !(flags_in & MIVQ_PQ_LEGACY_EXACT)) {
+        hipLaunchKernelGGL(pq_encode_exact_tiled_kernel, dim3((unsigned)ceil_div(n, kXRows), (unsigned)M),
+                           dim3(256), 0, st, x, n, d, M, L.dsub, ct, cn, u8);
+        int rc = check_launch("pq_encode_exact_tiled");
+        if (rc) return rc;
     } else {
         const size_t smem = (size_t)64 * (L.dsub + 1) * sizeof(float);
         MIVQ_REQUIRE(smem <= 160 * 1024, MIVQ_ERR_UNSUPPORTED, "pq_encode: dsub=%d too large", L.dsub);
@@ -827,7 +943,7 @@ extern "C" int mivq_kmeans_update(const float* x, int64_t n, int32_t d, int32_t 
                                   const uint8_t* assign, float* centroids, int32_t* counts, void* stream) {
     MIVQ_REQUIRE(M > 0 && d > 0 && n >= 0 && d % M == 0, MIVQ_ERR_INVALID, "kmeans_update: bad sizes");
     MIVQ_REQUIRE(ksub >= 1 && ksub <= 256, MIVQ_ERR_UNSUPPORTED, "kmeans_update: ksub=%d", ksub);
-    MIVQ_REQUIRE(d / M <= 256, MIVQ_ERR_UNSUPPORTED, "kmeans_update: dsub=%d > 256", d / M);
+    MIVQ_REQUIRE(d / M <= 256 * kKmDims, MIVQ_ERR_UNSUPPORTED, "kmeans_update: dsub=%d > %d", d / M, 256 * kKmDims);
     hipLaunchKernelGGL(kmeans_update_kernel, dim3(ksub, M), dim3(256), 0, as_stream(stream), x, n, d, M, ksub,
                        d / M, assign, centroids, counts);
     return check_launch("kmeans_update");

@@ -33,6 +33,7 @@ MIVQ_ERR_WORKSPACE = -4
 MIVQ_PQ_AUTO = 0
 MIVQ_PQ_FORCE_EXACT = 1
 MIVQ_PQ_LEGACY_MFMA = 2
+MIVQ_PQ_LEGACY_EXACT = 4
 METRIC_INNER_PRODUCT = 0
 METRIC_L2 = 1
 NO_ID = 0xFFFFFFFF

@@ -35,8 +35,9 @@ PQ_SHAPES = [
     (1000, 1536, 16, 8),    # MFMA KS=6 (the headline shape)
     (777, 1024, 16, 8),     # MFMA KS=4, ragged n
     (513, 1536, 32, 8),     # MFMA KS=3 (OPQ32 shape)
-    (300, 1024, 8, 8),      # wide filter KS=8 (dsub 128, 4 waves, codebook read from L2)
+    (300, 1024, 8, 8),      # wide filter KS=8 (dsub 128: K in two tile halves, 8 waves)
     (300, 1536, 8, 8),      # wide filter KS=12 (dsub 192: config #1's PQ8 at D=1536)
+    (300, 1280, 8, 8),      # wide filter KS=10 (dsub 160, K halves of 5 steps, generic load layout)
     (300, 1120, 8, 8),      # wide filter KS=9 (dsub 140, padded K)
     (200, 1024, 4, 8),      # dsub 256 (M = 4 at D = 1024: the sweep's `--pq-subquantizers 4`)
     (150, 1536, 4, 8),      # dsub 384 (M = 4 at D = 1536)
@@ -101,6 +102,25 @@ def test_pq_encode_bit_exact_trained_codebooks(dev, oracle, kind):
     np.testing.assert_array_equal(_h(_native.pq_encode(Xd, C, prep, 8, flags_extra=_native.MIVQ_PQ_LEGACY_MFMA)), ref)
     # the tiled exact kernel (register-blocked VALU GEMM, cross-lane argmin) on the same near-ties
     np.testing.assert_array_equal(_h(_native.pq_encode(Xd, C, prep, 8, exact=True)), ref)
+
+
+@pytest.mark.parametrize("n,d,M", [(60_001, 1536, 8), (40_000, 1536, 12), (40_000, 1280, 8), (20_000, 1120, 8)])
+def test_pq_encode_bit_exact_wide_subspaces(dev, oracle, n, d, M):
+    """Wide subspaces on k-means codebooks (thousands of resolve items per workgroup): dsub 192,
+    128, 160 run the K-halves filter (8 waves) and the resolve with rows in registers and the
+    full-batch candidate lists; dsub 140 the 4-wave filter and the generic resolve."""
+    from haag_vq import _native
+    from haag_vq.methods._kmeans import train_pq
+
+    rng = np.random.default_rng(d + M)
+    X = rng.standard_normal((n, d)).astype(np.float32)
+    X /= np.linalg.norm(X, axis=1, keepdims=True)
+    X[7] = X[3]  # duplicate rows
+    Xd = _t(X, dev)
+    C = train_pq(Xd[:16384], M, 8, niter=6)
+    ref = oracle.pq_encode(X, _h(C))
+    prep = _native.pq_prepare(C, 8)
+    np.testing.assert_array_equal(_h(_native.pq_encode(Xd, C, prep, 8)), ref)
 
 
 def test_pq_encode_bit_exact_config5_shape(dev, oracle):

@@ -3,9 +3,13 @@
 // library itself only instantiates V = 0.
 #include "../vector-quantization_amd/csrc/pq_encode_cs.hip"
 
+#ifndef CS_KS  // K-steps of the subspace shape (dsub = 16 CS_KS for the specialised kernels)
+#define CS_KS 6
+#endif
+
 #define VARIANT(v)                                                                                     \
     case v:                                                                                           \
-        return (int)mivq::launch_pq_encode_cs_v<6, v>(x, n, d, M, dsub, C, cn, img, hinit, bnd, pd, bnd2, codesT, items, \
+        return (int)mivq::launch_pq_encode_cs_v<CS_KS, v>(x, n, d, M, dsub, C, cn, img, hinit, bnd, pd, bnd2, codesT, items, \
                                                       counts, pinfo, (hipStream_t)st);
 
 extern "C" __attribute__((visibility("default"))) int cs_variant(int V, const float* x, int64_t n, int d, int M,

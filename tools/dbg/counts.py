@@ -1,6 +1,9 @@
-"""Per-workgroup resolve list sizes of one mivq_pq_encode call (1M x 1536 Gaussian, PQ16): the
-merged resolve's duration is that of its slowest workgroup, so max / mean of the per-workgroup
-work says how much of it is imbalance (run on the GPU box)."""
+"""Per-workgroup resolve list sizes of one mivq_pq_encode call (cs path): the merged resolve's
+duration is that of its slowest workgroup, so max / mean of the per-workgroup work says how much
+of it is imbalance, and the totals say how many row-subspaces the filter left (run on the GPU box).
+
+usage: python tools/dbg/counts.py [n] [d] [M]   (defaults 1000000 1536 16; Gaussian rows)
+"""
 import sys
 from pathlib import Path
 
@@ -14,27 +17,28 @@ from haag_vq import _native  # noqa: E402
 from haag_vq.methods._kmeans import train_pq  # noqa: E402
 from bench import synth  # noqa: E402
 
-n, d, M = 1_000_000, 1536, 16
+n = int(sys.argv[1]) if len(sys.argv) > 1 else 1_000_000
+d = int(sys.argv[2]) if len(sys.argv) > 2 else 1536
+M = int(sys.argv[3]) if len(sys.argv) > 3 else 16
 dev = _native.require_device()
 X = synth(n, d, 0, dev, kind="gaussian")
 C = train_pq(X[:65536], M, 8, niter=25, seed=1234).contiguous()
 prep = _native.pq_prepare(C, 8)
-codes = _native.pq_encode(X, C, prep, 8)
+lib = _native.load_library()
+nb = lib.mivq_pq_encode_workspace_bytes(n, d, M, 8)
+ws = torch.zeros(nb, dtype=torch.uint8, device=dev)  # counts of unused workgroups stay 0
+codes = torch.empty((n, M), dtype=torch.uint8, device=dev)
+_native._call("mivq_pq_encode", _native._ptr(X), n, d, M, 8, _native._ptr(C), _native._ptr(prep), _native._ptr(ws),
+              ws.numel(), _native._ptr(codes), 0, _native._stream())
 torch.cuda.synchronize()
-ws = _native.workspace(0, dev)
-al = lambda v: (v + 255) // 256 * 256  # noqa: E731
+al = lambda v: (v + 255) // 256 * 256  # noqa: E731 (mivq_pq_encode's workspace layout)
 off = al(n * M) + al(max(n * M * 8, (n + 31) // 32 * M * 4))
-cnt = ws[off: off + 8 * 4096].view(torch.int32).cpu().numpy().reshape(-1, 2)
-grid = int((cnt.sum(1) > 0).sum())
-cnt = cnt[:256]
-np_, nf = cnt[:, 0], cnt[:, 1]
+cnt = ws[off: off + al((n + 127) // 128 * M * 8)].view(torch.int32).cpu().numpy().reshape(-1, 2)
+used = cnt.sum(1) > 0
+np_, nf = cnt[used, 0], cnt[used, 1]
+print(f"n={n} d={d} M={M} dsub={d // M}: workgroups with items {int(used.sum())}")
+print(f"pair items {np_.sum()} ({np_.sum() / (n * M):.4%} of row-subspaces), "
+      f"full items {nf.sum()} ({nf.sum() / (n * M):.4%})")
+print(f"pairs per WG: mean {np_.mean():.0f} max {np_.max()}   full per WG: mean {nf.mean():.0f} max {nf.max()}")
 work = np_ / 32 * 1.0 + nf / 32 * 4.0  # pair batch ~1, full batch ~4 (relative cost)
-print("workgroups with items:", grid)
-print(f"pairs per WG: mean {np_.mean():.0f} min {np_.min()} max {np_.max()}")
-print(f"full  per WG: mean {nf.mean():.0f} min {nf.min()} max {nf.max()}")
 print(f"weighted work max/mean {work.max() / work.mean():.3f}")
-b = np.arange(256)
-m_of = (b >> 3) % M  # wg_coords_of when the grid is a multiple of 8 M
-for m in range(M):
-    sel = m_of == m
-    print(f"m={m:2d} pairs/WG {np_[sel].mean():7.0f}  full/WG {nf[sel].mean():7.0f}  work {work[sel].mean():6.1f}")

@@ -20,10 +20,10 @@ sys.path.insert(0, str(ROOT / "vector-quantization_amd"))
 # workload -> kernel-name substrings (template arguments select the shape)
 WORKLOADS = {
     "pq16_encode_1000000x1536_gaussian": ["pq_encode_cs_kernelILi6ELi3ELi0ELi96", "pq_resolve_merged_kernelILi6ELi96",
-                                          "pq_transpose_codes16_kernelILi16"],
+                                          "pq_transpose_codes16_kernel<16>"],
     "opq32_rotate_1000000x1536": ["opq_row_scale_kernel", "opq_split_gemm_kernel"],
     "sq8_encode_1000000x3072": ["sq_encode_f32_vec_kernel"],
-    "rabitq1_encode_1000000x3072": ["rabitq_encode_kernelILb0"],
+    "rabitq1_encode_1000000x3072": ["rabitq_encode_kernel<true>"],
 }
 
 

@@ -801,7 +801,9 @@ extern "C" size_t mivq_pq_encode_workspace_bytes(int64_t n, int32_t d, int32_t M
     // cs path: n*M uint2 resolve items; legacy MFMA path: its filter flags (never both)
     b += align_up(std::max((size_t)n * M * 8, (size_t)ceil_div(n, 32) * M * sizeof(uint32_t)), 256);
     b += align_up(cs_counts_bytes(n, M), 256);  // cs path: list counts per workgroup
-    b += align_up((size_t)n * M * 8, 256);      // cs path: per pair item {score gap, Xs}
+#ifdef MIVQ_CS_TIMESTAMPS
+    b += align_up((size_t)n * M * 8, 256);      // probe build: per-workgroup timestamps
+#endif
     return b;
 }
 
@@ -834,7 +836,13 @@ extern "C" int mivq_pq_encode(const float* x, int64_t n, int32_t d, int32_t M, i
     off += align_up(std::max((size_t)n * M * 8, (size_t)ceil_div(n, 32) * M * sizeof(uint32_t)), 256);
     void* counts = ws + off;
     off += align_up(cs_counts_bytes(n, M), 256);
+    // {score gap, Xs} per pair item feed only the round-1 pair kernel (profiling builds); the
+    // library's merged resolve re-derives what it needs, so no n*M*8-byte region here
+#ifdef MIVQ_CS_TIMESTAMPS
     void* pinfo = ws + off;
+#else
+    void* pinfo = nullptr;
+#endif
 
     const bool aligned = (reinterpret_cast<uintptr_t>(x) % 16 == 0) && (d % 4 == 0) && (L.dsub % 4 == 0);
     const bool exact_only = (flags_in & MIVQ_PQ_FORCE_EXACT) != 0;

@@ -39,6 +39,8 @@
 
 #include <math.h>
 
+#include <type_traits>
+
 namespace mivq {
 namespace {
 
@@ -51,6 +53,21 @@ typedef float f32x4 __attribute__((ext_vector_type(4)));
 
 #ifndef MIVQ_CS_WAVES
 #define MIVQ_CS_WAVES 12
+#endif
+#ifndef MIVQ_CS_ASPLIT
+#define MIVQ_CS_ASPLIT 1
+#endif
+#ifndef MIVQ_GC_DS  // wide-subspace resolve: rows in registers, centroid rows loaded whole
+#define MIVQ_GC_DS 1
+#endif
+#ifndef MIVQ_GC_WHOLE_ROW
+#define MIVQ_GC_WHOLE_ROW 0
+#endif
+#ifndef MIVQ_GC_LIST  // wide-subspace resolve: full-batch candidates chained one per lane
+#define MIVQ_GC_LIST 1
+#endif
+#ifndef MIVQ_GC_LIST_NC  // pieces of a centroid row in the list chains (dsub > 128)
+#define MIVQ_GC_LIST_NC 4
 #endif
 constexpr int kWaves = MIVQ_CS_WAVES;  // 768 threads, 3 waves per SIMD (profiling builds may override)
 constexpr int kDepth = 1;   // x blocks in flight per wave
@@ -198,21 +215,29 @@ constexpr int max_loads() {
 // workgroup into `counts`.
 // DS > 0: the kernel for sub-rows of exactly DS floats (the addresses and load counts fold
 // to constants); DS = 0 reads dsub at run time.
-template <int KS, int LAYOUT, int V = 0, int DS = 0, int NW = kWaves>
+// KH = 2 (wide subspaces with dsub == 16 KS, KS even): the wave's tile holds half of the
+// block's K at a time (the image's K-steps 0..KS/2-1, then the rest), so the tile is half as
+// wide and 8 waves fit next to the image; the B fragments of both halves stay in registers.
+// Image K-step g gives lane half h the dims 8 KS h + 8 g + [0, 8), so tile half hh holds the
+// dims hh 8 KT + [0, 8 KT) and 8 KS + hh 8 KT + [0, 8 KT) (KT = KS / 2): two 32 KT-byte
+// segments of each row.
+template <int KS, int LAYOUT, int V = 0, int DS = 0, int NW = kWaves, int KH = 1>
 __global__ __launch_bounds__(NW * 64) void pq_encode_cs_kernel(
     const float* __restrict__ x, int64_t n, int d, int M, int dsub_in, int64_t rows_per_wg,
     const float* __restrict__ C, const float* __restrict__ cn, const half8* __restrict__ img,
     const float* __restrict__ hinit, const float4* __restrict__ bnd, uint8_t* __restrict__ codesT,
     uint2* __restrict__ items, int2* __restrict__ counts, float2* __restrict__ pinfo,
     const float2* __restrict__ pdw, const float4* __restrict__ bnd2) {
+    static_assert(KH == 1 || (KH == 2 && KS % 2 == 0), "K halves");
     constexpr int FR = 8 * KS * 64;
-    constexpr int PITCH = 32 * KS + 16;  // bytes per fp16 tile row (16 B pad: conflict-free reads)
-    constexpr int NIMAX = LAYOUT == 0 ? max_loads<KS>() : 2 * KS;
+    constexpr int KT = KS / KH;          // K-steps per tile fill
+    constexpr int PITCH = 32 * KT + 16;  // bytes per fp16 tile row (16 B pad: conflict-free reads)
+    constexpr int NIMAX = LAYOUT == 0 ? max_loads<KT>() : 2 * KT;
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     half8* cimg = reinterpret_cast<half8*>(smem);
     unsigned char* stg_all = smem + FR * 16;
     constexpr int NT = NW * 64;
-    constexpr int kDep = NW >= kWaves ? kDepth : 2;  // x blocks in flight per wave
+    constexpr int kDep = (NW >= kWaves || KH > 1) ? kDepth : 2;  // x blocks in flight per wave
     float* hb = reinterpret_cast<float*>(stg_all + NW * 32 * PITCH);
     float* cnl = hb + 256;
     int* ctr = reinterpret_cast<int*>(cnl + 256);  // [0] pairs, [1] full, [2] resolve batches
@@ -252,7 +277,8 @@ __global__ __launch_bounds__(NW * 64) void pq_encode_cs_kernel(
     // rpi*q idle.  LAYOUT P in {1, 3}: the vb's 32*q chunks are read in order, 64 per
     // instruction, all lanes busy; the lane pattern repeats every P instructions (RP rows),
     // so P per-lane offsets suffice.
-    const int q = dsub >> 2;                 // 16-B chunks per row
+    const int dsub_h = dsub / KH;            // floats per tile fill (KH = 2: dsub == 16 KS)
+    const int q = dsub_h >> 2;               // 16-B chunks per row and tile fill
     const int XS = (V & 128) ? dsub : d;     // row stride of the loads (V&128: subspace-major probe)
     constexpr int PER = LAYOUT == 0 ? 1 : LAYOUT;
     const int rpi = LAYOUT == 0 ? min(32, 64 / q) : 64 * PER / q;  // rows per instruction / period
@@ -264,7 +290,8 @@ __global__ __launch_bounds__(NW * 64) void pq_encode_cs_kernel(
         const int c = LAYOUT == 0 ? l : 64 * sidx + l;
         prow[sidx] = c / q;
         const int col = c - prow[sidx] * q;
-        voff[sidx] = (prow[sidx] * XS + 4 * col) * 4;
+        const int gcol = KH == 1 ? 4 * col : 4 * col + (col >= 2 * KT ? 8 * KS - 8 * KT : 0);
+        voff[sidx] = (prow[sidx] * XS + gcol) * 4;
         toff[sidx] = prow[sidx] * PITCH + 8 * col;
     }
     if (LAYOUT == 0) lactive = l < rpi * q;
@@ -290,13 +317,13 @@ __global__ __launch_bounds__(NW * 64) void pq_encode_cs_kernel(
     auto ibase = [&](int i) { return LAYOUT == 0 ? rpi * i : rpi * (i / PER); };
     // One code path for every vb (no branches around the loads: divergent paths would make the
     // compiler join the prefetch registers with moves that wait for the loads right away).
-    auto load = [&](int vb, float4* dst) {
+    auto load = [&](int vb, int hh, float4* dst) {
 #pragma unroll
         for (int i = 0; i < NIMAX; ++i) {
             if (i < ni) {  // uniform
                 // the block's uniform offset goes in soffset (SALU; gfx950 range-checks
                 // voffset + soffset, tools/probes/soffset_range.hip), the lane's in voffset
-                const int so = (vb * 32 + ibase(i)) * XS * 4;
+                const int so = (vb * 32 + ibase(i)) * XS * 4 + hh * (8 * KT * 4);
                 const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(xr_rsrc, voff[i % PER], so, kXAux);
                 dst[i] = make_float4(__uint_as_float(v[0]), __uint_as_float(v[1]), __uint_as_float(v[2]),
                                      __uint_as_float(v[3]));
@@ -342,7 +369,7 @@ __global__ __launch_bounds__(NW * 64) void pq_encode_cs_kernel(
                 const int at = basep + __popcll(bp & below);
                 list[at] = make_uint2((uint32_t)prow, (uint32_t)pk);
                 // the legacy pair kernel's own window needs the score gap and Xs
-                if (pdw == nullptr) pinfo[(int64_t)m * n + r0 + at] = make_float2(pgap, pxs);
+                if (pdw == nullptr && pinfo != nullptr) pinfo[(int64_t)m * n + r0 + at] = make_float2(pgap, pxs);
             }
             if (isf) list[nrows - 1 - (basef + __popcll(bfull & below))] = make_uint2((uint32_t)frow, 0u);
         }
@@ -350,7 +377,12 @@ __global__ __launch_bounds__(NW * 64) void pq_encode_cs_kernel(
 
     // One step encodes block vb from registers xr and refills xr with block vb + kDep*NW
     // right after staging it, so kDep blocks per wave are in flight.
-    auto step = [&](const int vb, float4 (&xr)[NIMAX]) __attribute__((always_inline)) {
+    auto step = [&](const int vb, float4 (&xrh)[KH][NIMAX]) __attribute__((always_inline)) {
+        half8 bf[KS];
+        float xx = 0.0f;
+#pragma unroll
+        for (int hh = 0; hh < KH; ++hh) {
+        float4 (&xr)[NIMAX] = xrh[hh];
         // sigma * x -> fp16 -> this wave's tile (LAYOUT 0: lanes past the block's rows skip)
         // sigma == 1 (ordinary codebook magnitudes, pq_prep_mfma_kernel): no scaling multiply
         if (sigma == 1.0f) {
@@ -372,16 +404,15 @@ __global__ __launch_bounds__(NW * 64) void pq_encode_cs_kernel(
             }
         }
         lds_fence();
-        half8 bf[KS];
-        float xx = 0.0f;
 #pragma unroll
-        for (int ks = 0; ks < KS; ++ks) {
-            bf[ks] = *reinterpret_cast<const half8*>(stg + r * PITCH + h * (16 * KS) + 16 * ks);
-            const u32x4 u = __builtin_bit_cast(u32x4, bf[ks]);
+        for (int ks = 0; ks < KT; ++ks) {
+            bf[hh * KT + ks] = *reinterpret_cast<const half8*>(stg + r * PITCH + h * (16 * KT) + 16 * ks);
+            const u32x4 u = __builtin_bit_cast(u32x4, bf[hh * KT + ks]);
             xx = dot2_self(u[0], xx); xx = dot2_self(u[1], xx);
             xx = dot2_self(u[2], xx); xx = dot2_self(u[3], xx);
         }
-        if (vb + kDep * kProd < nvb && !((V & 64) && vb >= kProd)) load(vb + kDep * kProd, xr);
+        if (vb + kDep * kProd < nvb && !((V & 64) && vb >= kProd)) load(vb + kDep * kProd, hh, xr);
+        }
         xx += __shfl_xor(xx, 32);
 
         // Candidates: the 16 packed scores of centroid block cb in this lane form a group; each
@@ -400,10 +431,9 @@ __global__ __launch_bounds__(NW * 64) void pq_encode_cs_kernel(
         constexpr int NCB = (V & 16) ? 0 : (V & 32) ? 1 : 8;
         // MFMAs of centroid block cb+1 go into the other accumulator before the top-3 of cb
         // reads this one, so a wave's matrix and vector work overlap
+        // KH = 2: the A fragments in two halves (a scheduling barrier between them), so at most
+        // KS/2 of them are live next to the block's x registers
         auto scores = [&](int cb) __attribute__((always_inline)) {
-            half8 a[KS];
-#pragma unroll
-            for (int ks = 0; ks < KS; ++ks) a[ks] = cimg[(((V & 131072) ? 0 : cb) * KS + ks) * 64 + l];
             floatx16 acc;
 #pragma unroll
             for (int qq = 0; qq < 4; ++qq) {
@@ -411,8 +441,18 @@ __global__ __launch_bounds__(NW * 64) void pq_encode_cs_kernel(
                 acc[4 * qq + 0] = hv.x; acc[4 * qq + 1] = hv.y;
                 acc[4 * qq + 2] = hv.z; acc[4 * qq + 3] = hv.w;
             }
+            constexpr int NP = (KH > 1 && MIVQ_CS_ASPLIT) ? 2 : 1;
 #pragma unroll
-            for (int ks = 0; ks < KS; ++ks) acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(a[ks], bf[ks], acc, 0, 0, 0);
+            for (int part = 0; part < NP; ++part) {
+                half8 a[KS / NP];
+#pragma unroll
+                for (int ks = 0; ks < KS / NP; ++ks)
+                    a[ks] = cimg[(((V & 131072) ? 0 : cb) * KS + part * (KS / NP) + ks) * 64 + l];
+#pragma unroll
+                for (int ks = 0; ks < KS / NP; ++ks)
+                    acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(a[ks], bf[part * (KS / NP) + ks], acc, 0, 0, 0);
+                if (NP > 1 && part == 0) __builtin_amdgcn_sched_barrier(0);
+            }
             return acc;
         };
         if constexpr (NCB > 0) {
@@ -488,10 +528,13 @@ __global__ __launch_bounds__(NW * 64) void pq_encode_cs_kernel(
         }
     };
     {
-        float4 xa[NIMAX], xb[NIMAX];
+        float4 xa[KH][NIMAX], xb[KH][NIMAX];
         int vb = w;
-        if (vb < nvb) load(vb, xa);
-        if (kDep == 2 && vb + kProd < nvb) load(vb + kProd, xb);
+#pragma unroll
+        for (int hh = 0; hh < KH; ++hh) {
+            if (vb < nvb) load(vb, hh, xa[hh]);
+            if (kDep == 2 && vb + kProd < nvb) load(vb + kProd, hh, xb[hh]);
+        }
         for (; vb < nvb; vb += kDep * kProd) {
             step(vb, xa);
             if (kDep == 1) continue;
@@ -1241,9 +1284,22 @@ __device__ __forceinline__ int cswz(int k) { return (4 * KS) % 8 == 0 ? (k & 7) 
 template <int KS>
 constexpr bool merged_gc() { return KS > 6; }
 
+// GC full batches: the (row, centroid) candidates of a batch go to a per-wave LDS list of up
+// to kGcCap entries and are chained 64 at a time, one per lane (a lane-per-row loop would run
+// as many steps as the busiest lane has candidates, each an L2 round trip plus a dsub-long
+// chain); per-row (s, k) minima through 64-bit LDS atomics.
+constexpr int kGcCap = 4096;
+
 template <int KS>
 constexpr int merged_smem_bytes() {
-    return (merged_gc<KS>() ? 0 : 256 * 16 * KS * 4) + 2 * 256 * 4 + 16 + kMWaves * (32 * (16 * KS + 4) * 4);
+    return (merged_gc<KS>() ? 0 : 256 * 16 * KS * 4) + 2 * 256 * 4 + 16 + kMWaves * (32 * (16 * KS + 4) * 4) +
+           (merged_gc<KS>() && MIVQ_GC_LIST ? kMWaves * (32 * 8 + kGcCap * 2) : 0);
+}
+
+// float -> uint32 whose unsigned order is the float order (-0 == +0; NaN above everything)
+__device__ __forceinline__ uint32_t ord_key(float s) {
+    const uint32_t u = s == 0.0f ? 0u : __float_as_uint(s);
+    return s != s ? 0xFFFFFFFFu : (u & 0x80000000u) ? ~u : (u | 0x80000000u);
 }
 
 // V (profiling, tools/cs_variants.hip): 1 << 21 skips the full batches, 1 << 22 the pair
@@ -1272,6 +1328,12 @@ __global__ __launch_bounds__(kMWaves * 64) __attribute__((amdgpu_waves_per_eu(1,
     const int r = l & 31, h = l >> 5;
     float* xf = reinterpret_cast<float*>(reinterpret_cast<unsigned char*>(ctr + 4) +
                                          w * (32 * XP * 4));
+    // GC candidate lists (after the staging tiles): per wave 32 row keys, then kGcCap entries
+    unsigned long long* gkeys = reinterpret_cast<unsigned long long*>(
+                                    reinterpret_cast<unsigned char*>(ctr + 4) + kMWaves * (32 * XP * 4)) + w * 32;
+    unsigned short* glist = reinterpret_cast<unsigned short*>(
+                                reinterpret_cast<unsigned char*>(ctr + 4) + kMWaves * (32 * XP * 4) + kMWaves * 32 * 8) +
+                            w * kGcCap;
 
     int m;
     int64_t chunk;
@@ -1324,12 +1386,15 @@ __global__ __launch_bounds__(kMWaves * 64) __attribute__((amdgpu_waves_per_eu(1,
     // canonical score of centroid k for the row xv held in registers (DS > 0: the whole
     // centroid row is read first, then the sequential fmaf chain runs without waits)
     constexpr int NQ = DS > 0 ? DS / 4 : 1;
+    // GC (wide subspaces): the centroid row comes from C (L2) with all of its loads in flight
+    // at once (or half of them), so a chain waits for one or two L2 round trips instead of
+    // one per 16-B step
     auto exact_reg = [&](const f32x4 (&xv)[NQ], int k) __attribute__((always_inline)) {
-        const float* c = cl + k * CP;
-        const int sw = cswz<KS>(k);
+        const float* c = GC ? Cm + (int64_t)k * dsub : cl + k * CP;
+        const int sw = GC ? 0 : cswz<KS>(k);
         // the centroid row in two halves (register budget: the pair loop holds a prefetched
         // gather next to the row)
-        constexpr int NH = (NQ + 1) / 2;
+        constexpr int NH = (GC && MIVQ_GC_WHOLE_ROW) ? NQ : (NQ + 1) / 2;
         float dot = 0.0f;
 #pragma unroll
         for (int t0 = 0; t0 < NQ; t0 += NH) {
@@ -1352,6 +1417,33 @@ __global__ __launch_bounds__(kMWaves * 64) __attribute__((amdgpu_waves_per_eu(1,
     auto load_row = [&](const float* xr, f32x4 (&xv)[NQ]) __attribute__((always_inline)) {
 #pragma unroll
         for (int t = 0; t < NQ; ++t) xv[t] = *reinterpret_cast<const f32x4*>(xr + 4 * t);
+    };
+    // GC, DS > 0: canonical score of centroid k for the staged row xrr (LDS); the centroid row
+    // comes from C in NC pieces, each with all of its loads in flight (one L2 round trip per
+    // piece instead of one per 16-B step)
+    auto chain_gc = [&](auto nc_tag, const float* xrr, int k) __attribute__((always_inline)) {
+        constexpr int NC = decltype(nc_tag)::value;
+        constexpr int NP = (NQ + NC - 1) / NC;
+        const float* c = Cm + (int64_t)k * dsub;
+        float dot = 0.0f;
+#pragma unroll
+        for (int t0 = 0; t0 < NQ; t0 += NP) {
+            f32x4 cv[NP];
+#pragma unroll
+            for (int t = 0; t < NP; ++t)
+                if (t0 + t < NQ) cv[t] = *reinterpret_cast<const f32x4*>(c + 4 * (t0 + t));
+#pragma unroll
+            for (int t = 0; t < NP; ++t) {
+                if (t0 + t < NQ) {
+                    const f32x4 xq = *reinterpret_cast<const f32x4*>(xrr + 4 * (t0 + t));
+                    dot = __builtin_fmaf(xq.x, cv[t].x, dot);
+                    dot = __builtin_fmaf(xq.y, cv[t].y, dot);
+                    dot = __builtin_fmaf(xq.z, cv[t].z, dot);
+                    dot = __builtin_fmaf(xq.w, cv[t].w, dot);
+                }
+            }
+        }
+        return __builtin_fmaf(-2.0f, dot, cnl[k]);
     };
     // canonical score of centroid k for the staged row xr (sequential fmaf chain over t), any
     // dsub; GC: the centroid row straight from C (unswizzled)
@@ -1446,11 +1538,15 @@ __global__ __launch_bounds__(kMWaves * 64) __attribute__((amdgpu_waves_per_eu(1,
             }
         }
         if constexpr (GC) {
+            // the lane index through an opaque move: the 8 KS fragment addresses are formed
+            // here, per batch, not hoisted out of the batch loop (2 registers each)
+            int lv;
+            asm volatile("v_mov_b32 %0, %1" : "=v"(lv) : "v"(l));
 #pragma unroll
             for (int cb = 0; cb < 8; ++cb) {
                 half8 a1[KS];
 #pragma unroll
-                for (int ks = 0; ks < KS; ++ks) a1[ks] = im[(cb * KS + ks) * 64 + l];
+                for (int ks = 0; ks < KS; ++ks) a1[ks] = im[(cb * KS + ks) * 64 + lv];
 #pragma unroll
                 for (int ks = 0; ks < KS; ++ks)
                     acc[cb] = __builtin_amdgcn_mfma_f32_32x32x16_f16(a1[ks], bf[ks], acc[cb], 0, 0, 0);
@@ -1488,14 +1584,57 @@ __global__ __launch_bounds__(kMWaves * 64) __attribute__((amdgpu_waves_per_eu(1,
             for (int i = 0; i < 32; ++i) mm |= acc[2 * q2 + (i >> 4)][i & 15] >= thr ? (1u << i) : 0u;
             wm[q2] = bad ? 0xFFFFFFFFu : mm;
         }
+        if constexpr (GC && MIVQ_GC_LIST && DS > 0 && (V & (1 << 24)) == 0) {
+            // candidate list: lane prefix of the candidate counts, entries (row << 8) | k
+            const int cnt = r < cntb ? __popc(wm[0]) + __popc(wm[1]) + __popc(wm[2]) + __popc(wm[3]) : 0;
+            int inc = cnt;
+#pragma unroll
+            for (int o = 1; o < 64; o <<= 1) {
+                const int t = __shfl_up(inc, o);
+                if (l >= o) inc += t;
+            }
+            const int T = __builtin_amdgcn_readfirstlane(__shfl(inc, 63));
+            if (T <= kGcCap) {
+                if (l < 32) gkeys[l] = ~0ull;
+                int at = inc - cnt;
+                if (r < cntb) {
+#pragma unroll
+                    for (int q2 = 0; q2 < 4; ++q2) {
+                        uint32_t mm = wm[q2];
+                        while (mm) {
+                            const int bit = __builtin_ctz(mm);
+                            mm &= mm - 1u;
+                            const int cb = 2 * q2 + (bit >> 4), i = bit & 15;
+                            glist[at++] = (unsigned short)((r << 8) | (cb * 32 + (i & 3) + 8 * (i >> 2) + 4 * h));
+                        }
+                    }
+                }
+                lds_fence();
+                for (int base = 0; base < T; base += 64) {
+                    if (base + l < T) {
+                        const int e = glist[base + l];
+                        const int rr = e >> 8, k = e & 0xFF;
+                        const float sc = chain_gc(std::integral_constant<int, (DS > 128 ? MIVQ_GC_LIST_NC : 1)>{}, xf + rr * XP, k);
+                        atomicMin(&gkeys[rr], ((unsigned long long)ord_key(sc) << 32) | (unsigned)k);
+                    }
+                }
+                lds_fence();
+                if (h == 0 && r < cntb) {
+                    const unsigned long long key = gkeys[r];
+                    // (s, k) minimum; no finite-or--inf candidate (all NaN / +inf) -> 0, as below
+                    codesT[(int64_t)m * n + r0 + rowl] = (uint8_t)((uint32_t)(key >> 32) < 0xFF800000u ? (key & 0xFF) : 0);
+                }
+                return;
+            }
+        }
         float bs = INFINITY;
         int bk = 256;
         auto take = [&](float sc, int k) __attribute__((always_inline)) {
             if (sc < bs || (sc == bs && k < bk)) { bs = sc; bk = k; }
         };
         if (r < cntb && !(V & (1 << 24))) {
-            f32x4 xv[NQ];
-            if constexpr (DS > 0) load_row(xr, xv);
+            f32x4 xv[GC ? 1 : NQ];
+            if constexpr (DS > 0 && !GC) load_row(xr, xv);
             while ((wm[0] | wm[1] | wm[2] | wm[3]) != 0u) {
                 const int wi = wm[0] ? 0 : wm[1] ? 1 : wm[2] ? 2 : 3;
                 const uint32_t wsel = wm[0] ? wm[0] : wm[1] ? wm[1] : wm[2] ? wm[2] : wm[3];
@@ -1507,7 +1646,8 @@ __global__ __launch_bounds__(kMWaves * 64) __attribute__((amdgpu_waves_per_eu(1,
                 wm[3] = wi == 3 ? rest : wm[3];
                 const int cb = 2 * wi + (bit >> 4), i = bit & 15;
                 const int k = cb * 32 + (i & 3) + 8 * (i >> 2) + 4 * h;
-                if constexpr (DS > 0) take(exact_reg(xv, k), k);
+                if constexpr (GC && DS > 0) take(chain_gc(std::integral_constant<int, (DS > 128 ? 2 : 1)>{}, xr, k), k);
+                else if constexpr (DS > 0) take(exact_reg(xv, k), k);
                 else take(exact(xr, k), k);
             }
         }
@@ -1524,7 +1664,11 @@ __global__ __launch_bounds__(kMWaves * 64) __attribute__((amdgpu_waves_per_eu(1,
         const int kk = h ? k2 : k1;
         float sc = 0.0f;
         if (r < cntb) {
-            if constexpr (DS > 0) {
+            if constexpr (GC && DS > 0) {
+                // the next batch's gather is in flight (2 KS registers): the centroid row in
+                // two pieces when a whole one would not fit next to it
+                sc = chain_gc(std::integral_constant<int, (DS + 8 * KS > 200 ? 2 : 1)>{}, xr, kk);
+            } else if constexpr (DS > 0) {
                 f32x4 xv[NQ];
                 load_row(xr, xv);
                 sc = exact_reg(xv, kk);
@@ -1736,6 +1880,23 @@ hipError_t launch_pq_encode_cs_v(const float* x, int64_t n, int d, int M, int ds
             smem_launch = smem + (MIVQ_CS_D64_WAVES - NW) * 32 * (32 * KS + 16);
         }
     }
+#ifndef MIVQ_CS_WIDE_WAVES
+#define MIVQ_CS_WIDE_WAVES 8
+#endif
+#ifndef MIVQ_CS_WIDE_WAVES_KS8
+#define MIVQ_CS_WIDE_WAVES_KS8 MIVQ_CS_WIDE_WAVES
+#endif
+    // wide subspaces with dsub == 16 KS (128, 160, 192): the tile filled in two K halves, so 8
+    // waves fit next to the image instead of 4 (KH = 2 above)
+    if constexpr (KS >= 8 && KS % 2 == 0 && MIVQ_CS_WIDE_WAVES > 0 && (V & (1 << 21)) == 0) {
+        if (dsub == 16 * KS) {
+            constexpr int KT = KS / 2, NWW = KS == 8 ? MIVQ_CS_WIDE_WAVES_KS8 : MIVQ_CS_WIDE_WAVES;
+            constexpr int LH = (4 * KT == 24 || 4 * KT == 12) ? 3 : (4 * KT == 16 || 4 * KT == 32) ? 1 : 0;
+            kern = pq_encode_cs_kernel<KS, LH, V, 16 * KS, NWW, 2>;
+            nw_launch = NWW;
+            smem_launch = 8 * KS * 64 * 16 + NWW * 32 * (32 * KT + 16) + 2 * 256 * 4 + 16;
+        }
+    }
     hipError_t e = hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, smem_launch);
     if (e != hipSuccess) return e;
     const int cus = device_cus();
@@ -1755,9 +1916,13 @@ hipError_t launch_pq_encode_cs_v(const float* x, int64_t n, int d, int M, int ds
     if constexpr (!legacy) {
         constexpr int msmem = merged_smem_bytes<KS>();
         static_assert(msmem <= 160 * 1024, "merged resolve LDS");
+        // DS specialisations: the row held in registers for the chains (exact_reg); wide
+        // subspaces with dsub == 16 KS as well (their chains read C from L2)
+        constexpr bool wide_ds = KS >= 8 && KS % 2 == 0 && MIVQ_GC_DS;
         auto mkern = (KS == 6 && dsub == 96)   ? pq_resolve_merged_kernel<KS, (KS == 6 ? 96 : 0), V>
                      : (KS == 4 && dsub == 64) ? pq_resolve_merged_kernel<KS, (KS == 4 ? 64 : 0), V>
                      : (KS == 3 && dsub == 48) ? pq_resolve_merged_kernel<KS, (KS == 3 ? 48 : 0), V>
+                     : (wide_ds && dsub == 16 * KS) ? pq_resolve_merged_kernel<KS, (wide_ds ? 16 * KS : 0), V>
                                                : pq_resolve_merged_kernel<KS, 0, V>;
         e = hipFuncSetAttribute((const void*)mkern, hipFuncAttributeMaxDynamicSharedMemorySize, msmem);
         if (e != hipSuccess) return e;

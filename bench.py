@@ -19,7 +19,8 @@ Second-level legs (keys of the same JSON line):
              rows (BASELINE north_star "10M x 1536 at 1 GPU"), parity on a 200,000-row sample.
   config5    BASELINE configs[4], the MS MARCO shape: 6.65M x 1024 rows per GPU (53.2M over
              8 GPUs), PQ16 encode + ADC top-10 of 10,000 queries with the RCCL merge.
-  configs    (N = 1 only) configs[2] OPQ32 encode + ADC recall@10 (1M x 1536) and configs[3]
+  configs    (N = 1 only) the sweep's PQ8 shape at 1M x 1536 (dsub 192, BASELINE configs[0]),
+             configs[2] OPQ32 encode + ADC recall@10 (1M x 1536) and configs[3]
              SQ-8 / RaBitQ-1 encode + search (1M x 3072), each with its own roofline.
 
 Usage:  python bench.py [--gpus N] [--steps K] [--warmup W]
@@ -419,6 +420,26 @@ def opq32_cpu_baseline(X, Y, codes, A, C, target_s):
             "code_agreement_cpu_rotation": float((got == ref_cpu).mean())}
 
 
+def pq_wide_leg(a, dev, M, steps, warmup, cpu=True):
+    """The sweep's own PQ shape (BASELINE configs[0]: `vq-benchmark sweep --method pq` on 1536-d
+    dbpedia rows, M = 8 -> dsub 192): the wide-subspace filter (K in two tile halves) + resolve,
+    1M x 1536 Gaussian rows, parity against the oracle on a 200,000-row sample."""
+    d, n = 1536, a.n
+    X = synth(n, d, seed=3, dev=dev, kind="gaussian")
+    C = train_codebook(X, M, 8, 0, 1, dev)
+    codes, e = encode_leg(X, C, a, 0, 1, dev, steps, warmup)
+    pa = parity_check(X, C, codes, _oracle(), max_rows=200_000, fp64_rows=5000)[0] if cpu else None
+    del X, codes
+    return {"metric": f"PQ{M} encode vectors/sec, 1M×1536 fp32 (the sweep's PQ shape, BASELINE configs[0])",
+            "value": n / e["wall_s"], "unit": "vectors/s", "ms_per_step": e["wall_s"] * 1e3, "dtype": "f32",
+            "config": {"workload": f"pq{M}_encode_{n}x{d}", "M": M, "dsub": d // M, "nbits": 8, "data": "gaussian"},
+            "roofline": {"bound": "hbm", "achieved": e["achieved_gbs"], "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": e["achieved_gbs"] / HBM_PEAK_GBS, "bytes_per_vector": e["bytes_per_vector"],
+                         "kernel_ms": e["kernel_ms"],
+                         "kernel": "pq_encode_cs_kernel (K-halves filter, 8 waves) + pq_resolve_merged_kernel + transpose"},
+            "parity": pa}
+
+
 def flatcodes_leg(a, dev, kind, steps, warmup, cpu=True):
     d, n = 3072, a.n
     g = torch.Generator(device=dev)
@@ -650,7 +671,8 @@ def main():
     if head_only and not a.no_configs:
         configs = {}
         cb = not a.no_cpu_baseline
-        for name, fn in (("opq32", lambda: opq32_leg(a, dev, 3, 1, cpu=cb)),
+        for name, fn in (("pq8", lambda: pq_wide_leg(a, dev, 8, 10, 3, cpu=cb)),
+                         ("opq32", lambda: opq32_leg(a, dev, 3, 1, cpu=cb)),
                          ("sq8", lambda: flatcodes_leg(a, dev, "sq8", 5, 2, cpu=cb)),
                          ("rabitq1", lambda: flatcodes_leg(a, dev, "rabitq1", 5, 2, cpu=cb))):
             configs[name] = fn()

@@ -143,19 +143,29 @@ __device__ __forceinline__ void split2(float v, _Float16& hi, _Float16& lo) {
     lo = (_Float16)(v - (float)hi);
 }
 
-// Per-row scale of x: one wave per row.
+// Per-row scale of x: one wave per row; d % 4 == 0 and 16-B aligned rows (the prepared path):
+// 16-B loads, eight per lane in flight (round 2's dword loop waited on one 4-B load at a time).
 __global__ __launch_bounds__(256) void opq_row_scale_kernel(const float* __restrict__ x, int64_t n, int d,
-                                                            float* __restrict__ rs) {
+                                                                float* __restrict__ rs) {
     const int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
     const int l = threadIdx.x & 63;
     if (row >= n) return;
-    const float* xr = x + row * d;
+    const float4* xr = reinterpret_cast<const float4*>(x + row * d);
+    const int q = d >> 2;
     float m = 0.0f;
     bool bad = false;
-    for (int k = l; k < d; k += 64) {
-        const float v = xr[k];
-        bad |= !isfinite(v);
-        m = fmaxf(m, fabsf(v));
+    for (int j0 = l; j0 < q; j0 += 8 * 64) {
+        float4 v[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+            const int j = j0 + 64 * u;
+            v[u] = j < q ? xr[j] : make_float4(0.f, 0.f, 0.f, 0.f);
+        }
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+            bad |= !isfinite(v[u].x) || !isfinite(v[u].y) || !isfinite(v[u].z) || !isfinite(v[u].w);
+            m = fmaxf(m, fmaxf(fmaxf(fabsf(v[u].x), fabsf(v[u].y)), fmaxf(fabsf(v[u].z), fabsf(v[u].w))));
+        }
     }
     for (int o = 32; o > 0; o >>= 1) m = fmaxf(m, __shfl_xor(m, o));
     bad = __any(bad);
@@ -450,7 +460,8 @@ extern "C" int mivq_opq_rotate_prepared(const float* x, int64_t n, int32_t d, co
         const int64_t cn = std::min(kOpqChunk, n - c0);
         const float* xc = x + c0 * d;
         float* yc = y + c0 * d;
-        hipLaunchKernelGGL(opq_row_scale_kernel, dim3((unsigned)ceil_div(cn, 4)), dim3(256), 0, st, xc, cn, d, rs + c0);
+        hipLaunchKernelGGL(opq_row_scale_kernel, dim3((unsigned)ceil_div(cn, 4)), dim3(256), 0, st, xc, cn, d,
+                           rs + c0);
         int rc = check_launch("opq_row_scale");
         if (rc) return rc;
         // 256 x 256 tiles (512 threads, 160 KiB) wherever a row block spans at least one such

@@ -457,6 +457,14 @@ def flatcodes_leg(a, dev, kind, steps, warmup, cpu=True):
         bpv, kname = 4 * d + d // 8 + 8, "rabitq_encode_kernel"
     wall, dev_ms = timed(enc, steps, warmup)
     codes = enc()
+    # this box's streaming rates on the same bytes (torch device copy: read + write; sum: read):
+    # the spec peak is the roofline, these say how much of it a plain stream gets here
+    Y = torch.empty_like(X)
+    _, copy_ms = timed(lambda: Y.copy_(X), 5, 2)
+    del Y
+    _, read_ms = timed(lambda: X.sum(), 5, 2)
+    calib = {"copy_gbs": 2 * X.numel() * 4 / (copy_ms * 1e-3) / 1e9, "read_gbs": X.numel() * 4 / (read_ms * 1e-3) / 1e9,
+             "note": "torch Y.copy_(X) (read + write) and X.sum() (read) on the leg's input, same box"}
     Q = X[:100].contiguous()  # reference convention: the queries are the first database rows
     search = lambda: _native.flat_search(Q, dec(codes), 10)  # noqa: E731
     swall, _ = timed(search, 2, 1)
@@ -470,7 +478,8 @@ def flatcodes_leg(a, dev, kind, steps, warmup, cpu=True):
            "config": {"workload": f"{kind}_encode_{n}x{d}"},
            "roofline": {"bound": "hbm", "kernel": kname, "achieved": ach, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                         "frac": ach / HBM_PEAK_GBS, "bytes_per_vector": bpv, "kernel_ms": dev_ms,
-                        "traffic": traffic_from_profile(f"{kind}_encode_{n}x{d}")},
+                        "traffic": traffic_from_profile(f"{kind}_encode_{n}x{d}"),
+                        "box_stream_rates": calib, "frac_of_box_copy_rate": ach / calib["copy_gbs"]},
            "search": {"qps": 100 / swall, "nq": 100, "k": 10, "recall@10": rec(g_, r_),
                       "method": "decode + exact L2 scan of the reconstructions (the reference's flat search)"}}
     if kind == "rabitq1":  # RaBitQIndex: IndexRaBitQ estimator search (center = mean, qb = 4)

@@ -123,10 +123,15 @@ struct SplitTile {
     static constexpr int TM = 32 * WR * RB, TN = 32 * WC * CB;
     static constexpr int BUF = 2 * (TM + TN) * SPITCH;  // x hi, x lo, B hi, B lo planes
     static constexpr int SMEM = 2 * BUF;                // double-buffered
-    static_assert(TM * SBK / 4 == 4 * NT && 2 * TN * SBK / 8 == 4 * NT, "4 loads of each kind per thread");
+    static constexpr int U = TM * SBK / 4 / NT;          // 16-B loads of each kind per thread
+    static_assert(TM * SBK / 4 == U * NT && 2 * TN * SBK / 8 == U * NT && TM == TN, "loads per thread");
 };
 using TileS = SplitTile<2, 2, 2, 2>;  // 128 x 128, 256 threads, 80 KiB (two per CU)
 using TileL = SplitTile<4, 2, 2, 4>;  // 256 x 256, 512 threads, 160 KiB (half the L2 traffic per MFMA)
+// 256 x 256 with 4 waves of 128 x 128 (accumulators in AGPRs): 16 fragment reads per 48 MFMAs
+// instead of 12 per 24 (MIVQ_OPQ_TILE4).  Measured slower: 16.0 vs 14.8 ms per 1M x 1536 GEMM
+// (one wave per SIMD cannot hide the LDS and barrier latency that two do); not the default.
+using TileW = SplitTile<2, 2, 4, 4>;
 
 // Power-of-two scale 2^(14 - E) with max|v| = m 2^E, m in [0.5, 1); 1 for 0 / inf / NaN.
 // Clamped to fp32's normal exponents (rows below 2^-112 lose relative accuracy).
@@ -276,31 +281,32 @@ __global__ __launch_bounds__(WR * WC * 64) void opq_split_gemm_kernel(const floa
     const int c0 = (int)(t % ctiles) * TN;
     const int64_t dd = (int64_t)d * d;
 
-    // staging geometry: x: 4 float4 per thread (row e / 8, k 4 (e % 8)); B: 4 x 16 B per
+    // staging geometry: x: U float4 per thread (row e / 8, k 4 (e % 8)); B: U x 16 B per
     // thread (plane e / (4 TN), column (e % 4 TN) / 4, k 8 (e % 4))
-    float sx[4];
-    int xrow[4], xk[4];
+    constexpr int U = T::U;
+    float sx[U];
+    int xrow[U], xk[U];
 #pragma unroll
-    for (int u = 0; u < 4; ++u) {
+    for (int u = 0; u < U; ++u) {
         const int e = tid + NT * u;
         xrow[u] = e >> 3;
         xk[u] = 4 * (e & 7);
         const int64_t gr = r0 + xrow[u];
         sx[u] = gr < n ? rs[gr] : 0.0f;
     }
-    int bpl[4], bcol[4], bk[4];
+    int bpl[U], bcol[U], bk[U];
 #pragma unroll
-    for (int u = 0; u < 4; ++u) {
+    for (int u = 0; u < U; ++u) {
         const int e = tid + NT * u;
         bpl[u] = e / (4 * TN);
         bcol[u] = (e % (4 * TN)) >> 2;
         bk[u] = 8 * (e & 3);
     }
-    float4 xv[4];
-    uint4 bv[4];
+    float4 xv[U];
+    uint4 bv[U];
     auto gload = [&](int k0) __attribute__((always_inline)) {
 #pragma unroll
-        for (int u = 0; u < 4; ++u) {
+        for (int u = 0; u < U; ++u) {
             const int64_t gr = r0 + xrow[u];
             const int k = k0 + xk[u];
             xv[u] = (gr < n && k < d) ? *reinterpret_cast<const float4*>(x + gr * d + k) : make_float4(0.f, 0.f, 0.f, 0.f);
@@ -311,7 +317,7 @@ __global__ __launch_bounds__(WR * WC * 64) void opq_split_gemm_kernel(const floa
     };
     auto sstore = [&](unsigned char* buf) __attribute__((always_inline)) {
 #pragma unroll
-        for (int u = 0; u < 4; ++u) {
+        for (int u = 0; u < U; ++u) {
             half4 h, lo;
             const float v[4] = {xv[u].x * sx[u], xv[u].y * sx[u], xv[u].z * sx[u], xv[u].w * sx[u]};
 #pragma unroll
@@ -466,8 +472,14 @@ extern "C" int mivq_opq_rotate_prepared(const float* x, int64_t n, int32_t d, co
         if (rc) return rc;
         // 256 x 256 tiles (512 threads, 160 KiB) wherever a row block spans at least one such
         // tile; the 128 x 128 kernel for narrow matrices
-        rc = (d >= 256 && cn >= 256) ? launch_split<TileL, 4, 2, 2, 4>(xc, cn, d, rs + c0, bimg, hdr, yc, st)
-                                     : launch_split<TileS, 2, 2, 2, 2>(xc, cn, d, rs + c0, bimg, hdr, yc, st);
+#ifndef MIVQ_OPQ_TILE4
+#define MIVQ_OPQ_TILE4 0
+#endif
+        if (d >= 256 && cn >= 256)
+            rc = MIVQ_OPQ_TILE4 ? launch_split<TileW, 2, 2, 4, 4>(xc, cn, d, rs + c0, bimg, hdr, yc, st)
+                                : launch_split<TileL, 4, 2, 2, 4>(xc, cn, d, rs + c0, bimg, hdr, yc, st);
+        else
+            rc = launch_split<TileS, 2, 2, 2, 2>(xc, cn, d, rs + c0, bimg, hdr, yc, st);
         if (rc) return rc;
     }
     return MIVQ_OK;

@@ -20,6 +20,9 @@ inline hipStream_t as_stream(void* s) { return reinterpret_cast<hipStream_t>(s);
 // Returns MIVQ_ERR_HIP with the launch error if the last launch failed.
 int check_launch(const char* what);
 
+// CU count of the current device, cached per (thread, device) (pq_encode_cs.hip).
+int device_cus();
+
 #define MIVQ_REQUIRE(cond, code, ...)                          \
     do {                                                       \
         if (!(cond)) return ::mivq::set_error((code), __VA_ARGS__); \

@@ -1790,6 +1790,8 @@ __global__ __launch_bounds__(256) void pq_transpose_codes16_kernel(const uint8_t
     }
 }
 
+}  // namespace
+
 // CU count of the current device, cached per (thread, device): no shared mutable state.
 int device_cus() {
     constexpr int kMaxDev = 64;
@@ -1801,6 +1803,8 @@ int device_cus() {
     if (dev >= 0 && dev < kMaxDev) cache[dev] = cus;
     return cus;
 }
+
+namespace {
 
 // Chunk count for one workgroup per CU at a time: minimise the rounds of workgroups per row
 // (ceil(chunks*M / CUs) / chunks), preferring fewer chunks, with at least 32 nw rows each

@@ -121,3 +121,27 @@ def test_benchmark_index_compare_and_sweep_timestamps():
     assert list(df["method"]) == ["sq_flat"] and all(ISO_UTC.match(t) for t in df["timestamp"])
     df2 = sweep_bpd(lambda _b: FlatQuantizedIndex(ScalarQuantizer(num_bits=8)), [4.0, 8.0], X, Q, gt, k=3)
     assert list(df2["bpd"]) == [4.0, 8.0] and df2["timestamp"].nunique() == 1
+
+
+@pytest.mark.gpu
+def test_precompute_gt_cli_matches_numpy(tmp_path):
+    """`vq-benchmark precompute-gt` on a memory-mapped .npy: database streamed in slices (a short
+    last slice included) and merged on the device, equal to a numpy fp64 brute force."""
+    from typer.testing import CliRunner
+
+    from haag_vq.benchmarks import precompute_ground_truth as pg
+    from haag_vq.cli import app
+
+    X = _unit_rows(3000, 40, 9)
+    np.save(tmp_path / "v.npy", X)
+    ids, dists = pg.exact_knn_l2(X, X[:25], k=7, batch_size=10, slice_rows=1024)
+    d2 = ((X[:25, None, :].astype(np.float64) - X[None].astype(np.float64)) ** 2).sum(-1)
+    ref = np.argsort(d2, axis=1, kind="stable")[:, :7]
+    assert (ids[:, 0] == ref[:, 0]).all()
+    np.testing.assert_allclose(dists, np.take_along_axis(d2, ids, 1), rtol=1e-5, atol=1e-5)
+    assert (np.diff(dists, axis=1) >= 0).all()
+    r = CliRunner().invoke(app, ["precompute-gt", "--vectors-path", str(tmp_path / "v.npy"), "--output-path",
+                                 str(tmp_path / "gt" / "g.npy"), "--num-queries", "25", "--k", "7"])
+    assert r.exit_code == 0, r.output
+    np.testing.assert_array_equal(np.load(tmp_path / "gt" / "g.npy"), ids)
+    assert np.load(tmp_path / "gt" / "g.distances.npy").shape == (25, 7)

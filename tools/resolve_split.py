@@ -74,15 +74,20 @@ def main():
     run(0)
     torch.cuda.synchronize()
     print(f"M={a.M} dsub={dsub}: codes equal the library: {bool((codesT.t() == ref).all())}", flush=True)
-    for v, name in VARIANTS.items():
+    # interleaved: every round runs each variant once (the clock drifts between rounds)
+    times = {v: [] for v in VARIANTS}
+    for v in VARIANTS:
         run(v)
-        torch.cuda.synchronize()
-        ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(a.reps)]
-        for s, e in ev:
-            s.record(); run(v); e.record()
-        torch.cuda.synchronize()
-        ms = sorted(s.elapsed_time(e) for s, e in ev)[a.reps // 2]
-        print(f"V={v:#10x} {name:44s} {ms:7.3f} ms", flush=True)
+    torch.cuda.synchronize()
+    for _ in range(a.reps):
+        for v in VARIANTS:
+            s_, e_ = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            s_.record(); run(v); e_.record()
+            torch.cuda.synchronize()
+            times[v].append(s_.elapsed_time(e_))
+    for v, name in VARIANTS.items():
+        t = sorted(times[v])
+        print(f"V={v:#10x} {name:44s} median {t[len(t) // 2]:7.3f} ms  min {t[0]:7.3f}", flush=True)
 
 
 if __name__ == "__main__":

@@ -429,6 +429,7 @@ def pq_wide_leg(a, dev, M, steps, warmup, cpu=True):
     C = train_codebook(X, M, 8, 0, 1, dev)
     codes, e = encode_leg(X, C, a, 0, 1, dev, steps, warmup)
     pa = parity_check(X, C, codes, _oracle(), max_rows=200_000, fp64_rows=5000)[0] if cpu else None
+    cb = cpu_baseline(X, C, _oracle(), a.cpu_seconds / 2) if cpu else None
     del X, codes
     return {"metric": f"PQ{M} encode vectors/sec, 1M×1536 fp32 (the sweep's PQ shape, BASELINE configs[0])",
             "value": n / e["wall_s"], "unit": "vectors/s", "ms_per_step": e["wall_s"] * 1e3, "dtype": "f32",
@@ -437,7 +438,7 @@ def pq_wide_leg(a, dev, M, steps, warmup, cpu=True):
                          "frac": e["achieved_gbs"] / HBM_PEAK_GBS, "bytes_per_vector": e["bytes_per_vector"],
                          "kernel_ms": e["kernel_ms"],
                          "kernel": "pq_encode_cs_kernel (K-halves filter, 8 waves) + pq_resolve_merged_kernel + transpose"},
-            "parity": pa}
+            "parity": pa, **({"cpu_baseline": cb} if cb else {})}
 
 
 def flatcodes_leg(a, dev, kind, steps, warmup, cpu=True):

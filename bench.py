@@ -436,7 +436,8 @@ def pq_wide_leg(a, dev, M, steps, warmup, cpu=True):
             "config": {"workload": f"pq{M}_encode_{n}x{d}", "M": M, "dsub": d // M, "nbits": 8, "data": "gaussian"},
             "roofline": {"bound": "hbm", "achieved": e["achieved_gbs"], "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": e["achieved_gbs"] / HBM_PEAK_GBS, "bytes_per_vector": e["bytes_per_vector"],
-                         "kernel_ms": e["kernel_ms"],
+                         "kernel_ms": e["kernel_ms"], "traffic": traffic_from_profile(f"pq{M}_encode_{n}x{d}"),
+                         "traffic_note": "PMC HBM bytes of the filter + resolve launches (the code transpose, ~1 %, not included)",
                          "kernel": "pq_encode_cs_kernel (K-halves filter, 8 waves) + pq_resolve_merged_kernel + transpose"},
             "parity": pa, **({"cpu_baseline": cb} if cb else {})}
 

@@ -57,6 +57,9 @@ typedef float f32x4 __attribute__((ext_vector_type(4)));
 #ifndef MIVQ_CS_ASPLIT
 #define MIVQ_CS_ASPLIT 1
 #endif
+#ifndef MIVQ_CS_KH_CONTIG  // K halves as contiguous row halves (lane half h reads tile half h)
+#define MIVQ_CS_KH_CONTIG 1
+#endif
 #ifndef MIVQ_GC_DS  // wide-subspace resolve: rows in registers, centroid rows loaded whole
 #define MIVQ_GC_DS 1
 #endif
@@ -290,7 +293,7 @@ __global__ __launch_bounds__(NW * 64) void pq_encode_cs_kernel(
         const int c = LAYOUT == 0 ? l : 64 * sidx + l;
         prow[sidx] = c / q;
         const int col = c - prow[sidx] * q;
-        const int gcol = KH == 1 ? 4 * col : 4 * col + (col >= 2 * KT ? 8 * KS - 8 * KT : 0);
+        const int gcol = (KH == 1 || MIVQ_CS_KH_CONTIG) ? 4 * col : 4 * col + (col >= 2 * KT ? 8 * KS - 8 * KT : 0);
         voff[sidx] = (prow[sidx] * XS + gcol) * 4;
         toff[sidx] = prow[sidx] * PITCH + 8 * col;
     }
@@ -323,7 +326,7 @@ __global__ __launch_bounds__(NW * 64) void pq_encode_cs_kernel(
             if (i < ni) {  // uniform
                 // the block's uniform offset goes in soffset (SALU; gfx950 range-checks
                 // voffset + soffset, tools/probes/soffset_range.hip), the lane's in voffset
-                const int so = (vb * 32 + ibase(i)) * XS * 4 + hh * (8 * KT * 4);
+                const int so = (vb * 32 + ibase(i)) * XS * 4 + hh * ((MIVQ_CS_KH_CONTIG ? 16 : 8) * KT * 4);
                 const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(xr_rsrc, voff[i % PER], so, kXAux);
                 dst[i] = make_float4(__uint_as_float(v[0]), __uint_as_float(v[1]), __uint_as_float(v[2]),
                                      __uint_as_float(v[3]));
@@ -404,12 +407,28 @@ __global__ __launch_bounds__(NW * 64) void pq_encode_cs_kernel(
             }
         }
         lds_fence();
+        if constexpr (KH > 1 && MIVQ_CS_KH_CONTIG) {
+            // contiguous halves: tile half hh holds dims [hh dsub/2, (hh+1) dsub/2), which are
+            // exactly the dims of lane half h == hh for every image K-step (8 KS h + 8 g + j),
+            // so those lanes read all KS fragments from it (exec-masked, no VALU) and the row
+            // segment is read as two whole-line halves
+            if (h == hh) {
+#pragma unroll
+                for (int ks = 0; ks < KS; ++ks) {
+                    bf[ks] = *reinterpret_cast<const half8*>(stg + r * PITCH + 16 * ks);
+                    const u32x4 u = __builtin_bit_cast(u32x4, bf[ks]);
+                    xx = dot2_self(u[0], xx); xx = dot2_self(u[1], xx);
+                    xx = dot2_self(u[2], xx); xx = dot2_self(u[3], xx);
+                }
+            }
+        } else {
 #pragma unroll
         for (int ks = 0; ks < KT; ++ks) {
             bf[hh * KT + ks] = *reinterpret_cast<const half8*>(stg + r * PITCH + h * (16 * KT) + 16 * ks);
             const u32x4 u = __builtin_bit_cast(u32x4, bf[hh * KT + ks]);
             xx = dot2_self(u[0], xx); xx = dot2_self(u[1], xx);
             xx = dot2_self(u[2], xx); xx = dot2_self(u[3], xx);
+        }
         }
         if (vb + kDep * kProd < nvb && !((V & 64) && vb >= kProd)) load(vb + kDep * kProd, hh, xr);
         }

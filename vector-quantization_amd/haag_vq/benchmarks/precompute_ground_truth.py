@@ -37,10 +37,11 @@ def exact_knn_l2(vectors: np.ndarray, queries: np.ndarray, k: int, batch_size: i
     dist_out = np.empty((nq, k), dtype=np.float32)
     if nq == 0 or k == 0:
         return ids_out, dist_out
-    Qd = _arrays.to_device(np.ascontiguousarray(queries, dtype=np.float32))
+    Qd = _arrays.to_device(np.array(queries, dtype=np.float32, copy=True))
     parts_d, parts_i = [], []
     for s in range(0, n, slice_rows):
-        Xs = _arrays.to_device(np.ascontiguousarray(vectors[s:s + slice_rows], dtype=np.float32))
+        # a writable host copy of the slice (torch refuses to wrap a read-only memory map)
+        Xs = _arrays.to_device(np.array(vectors[s:s + slice_rows], dtype=np.float32, copy=True))
         kk = min(k, Xs.shape[0])
         d_b, i_b = [], []
         for q0 in range(0, nq, batch_size):

@@ -6,8 +6,8 @@ Mirrors /root/reference/src/haag_vq/benchmarks/precompute_ground_truth.py:14-129
 rank 3).  The reference builds a faiss IndexFlatL2 on the whole array; here the file is
 memory-mapped (``allow_pickle=False``) and the database is streamed to the device in row
 slices, each searched with ``mivq_flat_search`` and the per-slice lists merged with
-``mivq_topk_merge`` (deterministic (distance, id) order), so the host never holds a second copy
-and the device holds one slice plus the queries.  ``--use-gpu`` is accepted for the reference's
+``mivq_topk_merge`` (deterministic (distance, id) order), so the host holds one slice beyond
+the mapping and the device one slice plus the queries.  ``--use-gpu`` is accepted for the reference's
 command line; the search always runs on the MI355X.
 """
 

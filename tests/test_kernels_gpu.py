@@ -525,3 +525,18 @@ def test_rabitq_search_bit_exact(dev, oracle, nq, n, d, qb, k, metric):
     rd, ri = oracle.topk_rows(keys, k)
     np.testing.assert_array_equal(_h(ki).view(np.uint32), ri)
     np.testing.assert_array_equal(_h(kd), rd)
+
+
+def test_pq_encode_slices_large_calls(dev, oracle):
+    """Calls above 2^21 rows run as 2^21-row slices: rows on both sides of the slice boundary and
+    in the ragged last slice equal the oracle (and a second slice boundary, 2^22)."""
+    from haag_vq import _native
+
+    rng = np.random.default_rng(21)
+    n, d, M = (1 << 22) + 1001, 64, 16
+    X = rng.standard_normal((n, d), dtype=np.float32)
+    C = _codebook(rng, X[:4096], M, 256)
+    Cd = _t(C, dev)
+    got = _h(_native.pq_encode(_t(X, dev), Cd, _native.pq_prepare(Cd, 8), 8))
+    for lo, hi in ((0, 2000), ((1 << 21) - 3000, (1 << 21) + 3000), ((1 << 22) - 2000, n)):
+        np.testing.assert_array_equal(got[lo:hi], oracle.pq_encode(np.ascontiguousarray(X[lo:hi]), C))

@@ -21,7 +21,9 @@ Second-level legs (keys of the same JSON line):
              8 GPUs), PQ16 encode + ADC top-10 of 10,000 queries with the RCCL merge.
   configs    (N = 1 only) the sweep's PQ8 shape at 1M x 1536 (dsub 192, BASELINE configs[0]),
              configs[2] OPQ32 encode + ADC recall@10 (1M x 1536) and configs[3]
-             SQ-8 / RaBitQ-1 encode + search (1M x 3072), each with its own roofline.
+             SQ-8 / RaBitQ-1 encode + search (1M x 3072), each with its own roofline, and the
+             registry's `rabitq` route (Extended RaBitQ, 4 bits, 200k x 3072 encode + decode,
+             fp64 MFMA roofline of erq_rotate_kernel).
 
 Usage:  python bench.py [--gpus N] [--steps K] [--warmup W]
   --gpus N > 1 without WORLD_SIZE in the environment starts
@@ -59,6 +61,7 @@ HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md chip table (spec)
 SETTLE_MS = 60.0               # untimed busy time after the W warmup calls of an encode leg (timed())
 MFMA_F32_PEAK_TFS = 157.3      # dense fp32 matrix peak (same table)
 MFMA_F16_PEAK_TFS = 2516.6     # dense f16/bf16 matrix peak = 16 x fp32 (same table)
+MFMA_F64_PEAK_TFS = 78.6       # dense fp64 matrix peak (MI355X spec; not in the guide's table)
 LDS_PEAK_GBS = 256 * 256 * 2.4  # 256 CUs x 256 B/clk (ds_read_b128) x 2.4 GHz = 157 TB/s
 # rigorous relative bound on a canonical fp32 score difference (oracle header): 2 (2 g_96 + u)
 CLEAR_GAP = 3e-5
@@ -91,6 +94,7 @@ def parse(argv=None):
     ap.add_argument("--config5-rows", type=int, default=6_650_000, help="config #5 rows per GPU")
     ap.add_argument("--config5-nq", type=int, default=10_000)
     ap.add_argument("--opq-iters", type=int, default=4)
+    ap.add_argument("--erq-rows", type=int, default=200_000, help="Extended RaBitQ leg rows (D = 3072)")
     ap.add_argument("--exact", action="store_true", help="force the exact VALU encode path")
     ap.add_argument("--legacy", action="store_true", help="diagnostic: subspace-looping MFMA kernel")
     ap.add_argument("--dry-run", action="store_true", help="CPU/gloo rehearsal of the rank plumbing")
@@ -326,8 +330,12 @@ def adc_leg(X, C, codes, a, rank, world, dev, Q, k, gt_queries, reps=3, cpu=True
         rd, ri = O.adc_search(O.adc_lut(Qh, Cn), ch, k)
         dt = time.perf_counter() - t0
         ok = np.array_equal(ri, got[:nqs]) if nqs <= gq else None
-        out["cpu_baseline"] = {"value": nqs / dt, "unit": "queries/s", "cores": 1, "kind": "port",
-                               "sample": f"{nqs} queries x {n} codes, oracle adc_lut + adc_search (scalar C)",
+        # oracle_adc_lut / oracle_adc_search are OpenMP loops over queries
+        # (oracle/mivq_oracle.c:379,407): the threads that ran are min(OpenMP threads, queries)
+        threads = min(O.cpu_threads(), nqs)
+        out["cpu_baseline"] = {"value": nqs / dt, "unit": "queries/s", "cores": threads, "kind": "port",
+                               "sample": f"{nqs} queries x {n} codes, oracle adc_lut + adc_search "
+                                         f"(C, OpenMP over queries, {threads} threads), {dt:.1f} s wall",
                                "ids_equal_gpu": ok}
     return out
 
@@ -535,6 +543,101 @@ def flatcodes_cpu_baseline(kind, X, codes, lo, den, target_s):
             "sample": f"first {n_s} rows, {how}, {dt:.1f} s wall", "codes_equal_gpu": equal}
 
 
+def extrabitq_leg(a, dev, steps, warmup, cpu=True):
+    """The registry's `rabitq` route (method_registry_saq.py:45-48 -> ExtendedRaBitQuantizer,
+    extended_rabitq.py:125-199): B-bit encode + decode of synthetic Gaussian rows at D = 3072.
+    A step is one round trip (compress + decompress); the roofline is erq_rotate_kernel's fp64
+    MFMA GEMM (2 D^2 FLOP per vector per direction), timed alone with HIP events on the stream
+    it runs on.  CPU baseline: the reference's numpy algorithm (oracle.extrabitq_encode, fp64
+    BLAS matmul) on a bounded sample, BLAS threads pinned with threadpoolctl."""
+    from haag_vq.methods.extended_rabitq import ExtendedRaBitQuantizer
+
+    d, n, nbits = 3072, a.erq_rows, 4
+    g = torch.Generator(device=dev)
+    g.manual_seed(5)
+    X = torch.randn((n, d), generator=g, device=dev, dtype=torch.float32)
+    t0 = time.perf_counter()
+    q = ExtendedRaBitQuantizer(num_bits=nbits, seed=0)
+    q.fit(X)
+    c, P, lv = q._state()
+    t_fit = time.perf_counter() - t0
+    codes = q.compress(X)
+    wall, dev_ms = timed(lambda: q.decompress(q.compress(X)), steps, warmup)
+    _, enc_ms = timed(lambda: q.compress(X), steps, 1)
+    o = torch.randn((n, d), generator=g, device=dev, dtype=torch.float64)
+    _, rot_ms = timed(lambda: _native.extrabitq_rotate(o, P, False), steps, 1)
+    _, rotT_ms = timed(lambda: _native.extrabitq_rotate(o, P, True), steps, 1)
+    del o
+    flops = 2.0 * n * d * d
+    tfs = flops / (rot_ms * 1e-3) / 1e12
+    xh = q.decompress(codes)
+    rel = float(((xh.double() - X.double()).norm(dim=1) / X.double().norm(dim=1)).mean())
+    out = {"metric": "Extended RaBitQ (registry `rabitq`) encode+decode vectors/sec, 3072-d fp32",
+           "value": n / wall, "unit": "vectors/s", "ms_per_step": wall * 1e3, "dtype": "f64",
+           "config": {"workload": f"extrabitq{nbits}_roundtrip_{n}x{d}", "num_bits": nbits, "fit_s": t_fit,
+                      "encode_ms": enc_ms, "step": "compress + decompress"},
+           "roofline": {"bound": "mfma", "kernel": "erq_rotate_kernel (v_mfma_f64_16x16x4_f64, o . P)",
+                        "achieved": tfs, "peak": MFMA_F64_PEAK_TFS, "unit": "TFLOP/s", "frac": tfs / MFMA_F64_PEAK_TFS,
+                        "rotate_ms": rot_ms, "rotate_transposed_ms": rotT_ms, "flops_per_launch": flops,
+                        "flops_per_vector": 2 * d * d,
+                        "peak_note": "MI355X dense fp64 matrix spec (78.6 TF); not in the microarch guide's table"},
+           "reconstruction_rel_err_mean": rel}
+    if cpu:
+        out["cpu_baseline"] = extrabitq_cpu_baseline(X, codes, q, a.cpu_seconds / 2)
+    del X, codes, xh
+    return out
+
+
+def extrabitq_cpu_baseline(X, codes, q, target_s):
+    """extended_rabitq.py:125-170 in numpy on the host cores (oracle.extrabitq_encode: fp64 BLAS
+    rotation), on a bounded sample of the same rows.  The sample's GPU indices must equal the CPU's
+    except where s sits on a level midpoint (fp64 summation order: tests/test_pinning_gpu.py)."""
+    from threadpoolctl import threadpool_limits
+
+    O = _oracle()
+    threads = O.cpu_threads()
+    nb = q.num_bits
+    fn = lambda xs: O.extrabitq_encode(xs, q.c, q.P, q.levels, nb)  # noqa: E731
+    with threadpool_limits(limits=threads):
+        n_cal = 500
+        t0 = time.perf_counter()
+        fn(X[:n_cal].cpu().numpy())
+        dt = time.perf_counter() - t0
+        n_s = int(min(X.shape[0], max(n_cal, n_cal * target_s / max(dt, 1e-6))))
+        Xs = X[:n_s].cpu().numpy()
+        t0 = time.perf_counter()
+        ref = fn(Xs)
+        dt = time.perf_counter() - t0
+    got = codes[:n_s].cpu().numpy()
+    D = Xs.shape[1]
+    ib = (D * nb + 7) // 8
+
+    def unpack(cb):
+        bits = np.unpackbits(cb[:, :ib], axis=1)[:, :D * nb].reshape(len(cb), D, nb)
+        return (bits.astype(np.int64) << np.arange(nb - 1, -1, -1)).sum(-1)
+
+    gi, ri = unpack(got), unpack(ref)
+    bad = np.argwhere(gi != ri)
+    ties = 0
+    if len(bad):
+        Xb = Xs[np.unique(bad[:, 0])].astype(np.float64)
+        rows = {r: i for i, r in enumerate(np.unique(bad[:, 0]))}
+        r_ = Xb - q.c
+        o_ = r_ / np.maximum(np.linalg.norm(r_, axis=1), 1e-12)[:, None]
+        s_ = (o_ @ q.P) * np.sqrt(D)
+        mids = 0.5 * (q.levels[:-1] + q.levels[1:])
+        for i, j in bad:
+            v = s_[rows[i], j]
+            ties += int(np.min(np.abs(mids - v)) <= 1e-12 * max(1.0, abs(v)) and abs(int(gi[i, j]) - int(ri[i, j])) == 1)
+    f_g, f_r = got[:, ib:].copy().view(np.float32), ref[:, ib:].copy().view(np.float32)
+    return {"value": n_s / dt, "unit": "vectors/s (encode)", "cores": threads, "kind": "port",
+            "sample": f"first {n_s} rows, oracle.extrabitq_encode (numpy fp64, BLAS on {threads} threads via "
+                      f"threadpoolctl), {dt:.1f} s wall",
+            "index_mismatches": int(len(bad)), "index_mismatches_that_are_midpoint_ties": ties,
+            "indices_compared": int(gi.size),
+            "factors_max_rel_diff": float(np.max(np.abs(f_g - f_r) / np.maximum(np.abs(f_r), 1e-30)))}
+
+
 def config5_leg(a, rank, world, dev, steps, warmup):
     """BASELINE configs[4]: 53.2M x 1024 row-sharded (6.65M rows per GPU), PQ16 + ADC top-10."""
     n, d, M = a.config5_rows, 1024, 16
@@ -685,7 +788,8 @@ def main():
         for name, fn in (("pq8", lambda: pq_wide_leg(a, dev, 8, 10, 3, cpu=cb)),
                          ("opq32", lambda: opq32_leg(a, dev, 3, 1, cpu=cb)),
                          ("sq8", lambda: flatcodes_leg(a, dev, "sq8", 5, 2, cpu=cb)),
-                         ("rabitq1", lambda: flatcodes_leg(a, dev, "rabitq1", 5, 2, cpu=cb))):
+                         ("rabitq1", lambda: flatcodes_leg(a, dev, "rabitq1", 5, 2, cpu=cb)),
+                         ("extrabitq4", lambda: extrabitq_leg(a, dev, 3, 1, cpu=cb))):
             configs[name] = fn()
             torch.cuda.empty_cache()
             log(f"[rank 0] {name}: {configs[name]}")

@@ -24,7 +24,7 @@ def _run(*args):
     return json.loads(lines[0])
 
 
-@pytest.mark.parametrize("n", [1, 2, 3])
+@pytest.mark.parametrize("n", [1, 2, 3, 8])
 def test_launcher_dry_run(n):
     out = _run("--gpus", str(n), "--dry-run")
     assert out["n_gpus"] == n

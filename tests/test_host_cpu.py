@@ -131,22 +131,52 @@ def _free_port():
     return p
 
 
-def test_exchange_topk_gloo_world2_matches_single_rank():
+def _exchange(X, Q, k, world):
+    ctx = mp.get_context("spawn")
+    out = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, X, Q, k, out)) for r in range(world)]
+    for p in procs:
+        p.start()
+    gd, gi = out.get(timeout=240)
+    for p in procs:
+        p.join(timeout=240)
+        assert p.exitcode == 0
+    return gd, gi
+
+
+def _single_rank(X, Q, k):
+    d2 = ((Q[:, None, :] - X[None, :, :]) ** 2).sum(-1)
+    ref = np.lexsort((np.broadcast_to(np.arange(X.shape[0]), d2.shape), d2))[:, :k]
+    return np.take_along_axis(d2, ref, 1).astype(np.float32), ref
+
+
+@pytest.mark.parametrize("world", [2, 8])
+def test_exchange_topk_gloo_matches_single_rank(world):
+    """world 8 = the node's GPU count; gloo stands in for RCCL on CPU tensors."""
     rng = np.random.default_rng(3)
     X = rng.standard_normal((501, 16))
     Q = rng.standard_normal((7, 16))
     k = 10
-    ctx = mp.get_context("spawn")
-    out = ctx.Queue()
-    port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, 2, port, X, Q, k, out)) for r in range(2)]
-    for p in procs:
-        p.start()
-    gd, gi = out.get(timeout=120)
-    for p in procs:
-        p.join(timeout=120)
-        assert p.exitcode == 0
-    d2 = ((Q[:, None, :] - X[None, :, :]) ** 2).sum(-1)
-    ref = np.lexsort((np.broadcast_to(np.arange(X.shape[0]), d2.shape), d2))[:, :k]
-    np.testing.assert_array_equal(gi.astype(np.int64), ref)
-    np.testing.assert_allclose(gd, np.take_along_axis(d2, ref, 1).astype(np.float32), rtol=0, atol=0)
+    gd, gi = _exchange(X, Q, k, world)
+    rd, ri = _single_rank(X, Q, k)
+    np.testing.assert_array_equal(gi.astype(np.int64), ri)
+    np.testing.assert_allclose(gd, rd, rtol=0, atol=0)
+
+
+def test_exchange_topk_gloo_world8_ties_across_shards():
+    """Every database row repeated in all 8 shards: each query's nearest distances occur once per
+    shard, so the merged top-k must take the (dist, id) order of mivq_topk_merge — equal
+    distances by increasing global id — exactly as one rank over all rows would."""
+    rng = np.random.default_rng(11)
+    base = rng.standard_normal((63, 8))
+    X = np.tile(base, (8, 1))  # shard r (63 rows at world 8) holds a copy of every base row
+    Q = rng.standard_normal((5, 8))
+    k = 20
+    gd, gi = _exchange(X, Q, k, 8)
+    rd, ri = _single_rank(X, Q, k)
+    np.testing.assert_array_equal(gi.astype(np.int64), ri)
+    np.testing.assert_array_equal(gd, rd)
+    # the first 8 entries of each query are one base row's 8 copies, in increasing id order
+    assert np.all(ri[:, :8] % 63 == ri[:, :1] % 63)
+    assert np.all(np.diff(ri[:, :8], axis=1) == 63)

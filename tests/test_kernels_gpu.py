@@ -407,6 +407,24 @@ def test_adc_bit_exact(dev, oracle, nq, n, d, M, nbits, k, metric):
     np.testing.assert_array_equal(_h(ii).view(np.uint32), i_ref)
 
 
+@pytest.mark.parametrize("offset", [1, 2, 3])
+def test_adc_lut_misaligned_centroids(dev, oracle, offset):
+    """A centroid tensor that starts off a 16-B boundary (a view with storage_offset % 4 != 0,
+    or a C-API caller's pointer): the LUT kernel takes its dword path instead of 16-B loads."""
+    from haag_vq import _native
+
+    rng = np.random.default_rng(40 + offset)
+    M, dsub, nq = 16, 96, 40
+    C = rng.standard_normal((M, 256, dsub)).astype(np.float32)
+    Q = rng.standard_normal((nq, M * dsub)).astype(np.float32)
+    flat = torch.zeros(C.size + offset, dtype=torch.float32, device=dev)
+    flat[offset:] = _t(C.reshape(-1), dev)
+    Cv = flat[offset:].view(M, 256, dsub)
+    assert Cv.data_ptr() % 16 != 0
+    for metric in (1, 0):
+        np.testing.assert_array_equal(_h(_native.adc_lut(_t(Q, dev), Cv, 8, metric)), oracle.adc_lut(Q, C, metric))
+
+
 @pytest.mark.parametrize("nq,n,d,k", [
     (20, 3000, 1024, 10), (7, 500, 37, 100), (4, 3, 16, 5),    # streaming scan
     (100, 20000, 96, 10),                                         # tiled, one chunk, 5 segments
@@ -525,6 +543,24 @@ def test_rabitq_search_bit_exact(dev, oracle, nq, n, d, qb, k, metric):
     rd, ri = oracle.topk_rows(keys, k)
     np.testing.assert_array_equal(_h(ki).view(np.uint32), ri)
     np.testing.assert_array_equal(_h(kd), rd)
+
+
+@pytest.mark.parametrize("d", [96, 192])
+def test_pq_encode_slice_boundary_wide_shapes(dev, oracle, d):
+    """the 2^21-row slicing at the shapes it was tuned for — dsub 96 (KS 6, the D96
+    wave count) and dsub 192 (KS 12, K-halves filter) with M = 1 — rows on both sides of the
+    boundary and the ragged last slice (1001 rows: the generic code transpose) vs the oracle."""
+    from haag_vq import _native
+
+    rng = np.random.default_rng(d)
+    n = (1 << 21) + 1001
+    Xd = torch.randn((n, d), device=dev, generator=torch.Generator(device=dev).manual_seed(d))
+    X0 = _h(Xd[:4096])
+    C = _codebook(rng, X0, 1, 256)
+    Cd = _t(C, dev)
+    got = _h(_native.pq_encode(Xd, Cd, _native.pq_prepare(Cd, 8), 8))
+    for lo, hi in ((0, 1500), ((1 << 21) - 2500, n)):
+        np.testing.assert_array_equal(got[lo:hi], oracle.pq_encode(_h(Xd[lo:hi]), C))
 
 
 def test_pq_encode_slices_large_calls(dev, oracle):

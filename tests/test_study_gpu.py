@@ -145,3 +145,17 @@ def test_precompute_gt_cli_matches_numpy(tmp_path):
     assert r.exit_code == 0, r.output
     np.testing.assert_array_equal(np.load(tmp_path / "gt" / "g.npy"), ids)
     assert np.load(tmp_path / "gt" / "g.distances.npy").shape == (25, 7)
+
+
+@pytest.mark.gpu
+def test_precompute_gt_pads_k_beyond_database():
+    """k > rows keeps the requested width like faiss IndexFlatL2.search: the real
+    neighbours first, then id -1 with distance FLT_MAX."""
+    from haag_vq.benchmarks import precompute_ground_truth as pg
+
+    X = _unit_rows(6, 16, 3)
+    ids, dists = pg.exact_knn_l2(X, X[:4], k=10, batch_size=3, slice_rows=4)
+    assert ids.shape == (4, 10) and dists.shape == (4, 10)
+    assert (ids[:, 6:] == -1).all() and (dists[:, 6:] == np.finfo(np.float32).max).all()
+    assert (np.sort(ids[:, :6], axis=1) == np.arange(6)).all()
+    assert (ids[:, 0] == np.arange(4)).all()

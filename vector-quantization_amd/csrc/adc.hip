@@ -31,7 +31,7 @@ constexpr int kLutQ = 32;
 
 __global__ __launch_bounds__(256) void adc_lut_kernel(const float* __restrict__ q, int64_t nq, int d, int M, int ksub,
                                                        int dsub, const float* __restrict__ C, int metric,
-                                                       float* __restrict__ lut) {
+                                                       int vec16, float* __restrict__ lut) {
     extern __shared__ __attribute__((aligned(16))) float qs[];  // [kLutQ][dsub]
     const int m = blockIdx.x;
     const int64_t q0 = (int64_t)blockIdx.y * kLutQ;
@@ -66,7 +66,7 @@ __global__ __launch_bounds__(256) void adc_lut_kernel(const float* __restrict__ 
             }
         }
     };
-    if ((dsub & 3) == 0) {
+    if (vec16) {  // dsub % 4 == 0 and C 16-B aligned (host-side test: views may start anywhere)
         // 16-B loads of the centroid row, the next one in flight while this one is used.  (Round
         // 2 replaced these by dword loads while chasing a two-stream mismatch in lanes 48..63;
         // the cause was the LDS-DMA OPQ GEMM on the other stream corrupting packed-fp32 results,
@@ -605,7 +605,8 @@ extern "C" int mivq_adc_lut(const float* q, int64_t nq, int32_t d, int32_t M, in
     const size_t smem = (size_t)kLutQ * (d / M) * sizeof(float);
     MIVQ_REQUIRE(smem <= 64 * 1024, MIVQ_ERR_UNSUPPORTED, "adc_lut: dsub=%d too large", d / M);
     hipLaunchKernelGGL(adc_lut_kernel, dim3((unsigned)M, (unsigned)ceil_div(nq, kLutQ)), dim3(256), smem,
-                       as_stream(stream), q, nq, d, M, ksub, d / M, centroids, metric, lut);
+                       as_stream(stream), q, nq, d, M, ksub, d / M, centroids, metric,
+                       (d / M) % 4 == 0 && reinterpret_cast<uintptr_t>(centroids) % 16 == 0 ? 1 : 0, lut);
     return check_launch("adc_lut");
 }
 

@@ -84,9 +84,11 @@ __global__ __launch_bounds__(256) void pairwise_kernel(const float* __restrict__
         for (int j = 0; j < 4; ++j) ys[b][4 * q4 + j][row] = py[j];
     };
 
-    float2v acc[8][2];
+    // scalar fp32 chains: packed fp32 math must not consume LDS-loaded registers (DESIGN.md §8,
+    // tools/isa_audit.py)
+    float acc[8][4];
 #pragma unroll
-    for (int i = 0; i < 8; ++i) acc[i][0] = acc[i][1] = (float2v){0.0f, 0.0f};
+    for (int i = 0; i < 8; ++i) acc[i][0] = acc[i][1] = acc[i][2] = acc[i][3] = 0.0f;
 
     fetch(0);
     stash(0);
@@ -101,17 +103,17 @@ __global__ __launch_bounds__(256) void pairwise_kernel(const float* __restrict__
             const f32x4 xb = *reinterpret_cast<const f32x4*>(&xs[b][t][ty * 8 + 4]);
             const f32x4 yv = *reinterpret_cast<const f32x4*>(&ys[b][t][tx * 4]);
             const float xv[8] = {xa.x, xa.y, xa.z, xa.w, xb.x, xb.y, xb.z, xb.w};
-            const float2v y01 = {yv.x, yv.y}, y23 = {yv.z, yv.w};
+            const float yy[4] = {yv.x, yv.y, yv.z, yv.w};
 #pragma unroll
             for (int i = 0; i < 8; ++i) {
-                const float2v xx = {xv[i], xv[i]};
-                if (IP) {
-                    acc[i][0] = __builtin_elementwise_fma(xx, y01, acc[i][0]);
-                    acc[i][1] = __builtin_elementwise_fma(xx, y23, acc[i][1]);
-                } else {
-                    const float2v d0 = xx - y01, d1 = xx - y23;
-                    acc[i][0] = __builtin_elementwise_fma(d0, d0, acc[i][0]);
-                    acc[i][1] = __builtin_elementwise_fma(d1, d1, acc[i][1]);
+#pragma unroll
+                for (int j = 0; j < 4; ++j) {
+                    if (IP) {
+                        acc[i][j] = __builtin_fmaf(xv[i], yy[j], acc[i][j]);
+                    } else {
+                        const float df = __fsub_rn(xv[i], yy[j]);
+                        acc[i][j] = __builtin_fmaf(df, df, acc[i][j]);
+                    }
                 }
             }
         }
@@ -126,7 +128,7 @@ __global__ __launch_bounds__(256) void pairwise_kernel(const float* __restrict__
     for (int i = 0; i < 8; ++i) {
         const int64_t gr = r0 + ty * 8 + i;
         if (gr >= n) continue;
-        f32x4 v = {acc[i][0].x, acc[i][0].y, acc[i][1].x, acc[i][1].y};
+        f32x4 v = {acc[i][0], acc[i][1], acc[i][2], acc[i][3]};
         if (IP) v = -v;
         float* o = out + gr * m + gc;
         if ((m & 3) == 0 && gc + 3 < m) {

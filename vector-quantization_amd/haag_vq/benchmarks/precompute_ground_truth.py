@@ -25,16 +25,21 @@ _SLICE_ROWS = 1 << 18
 
 def exact_knn_l2(vectors: np.ndarray, queries: np.ndarray, k: int, batch_size: int = 1000,
                  slice_rows: int = _SLICE_ROWS):
-    """(ids int64 (nq, k), squared L2 distances float32 (nq, k)), best first; k <= len(vectors)."""
+    """(ids int64 (nq, k), squared L2 distances float32 (nq, k)), best first.
+
+    k > len(vectors) keeps the requested width, as faiss IndexFlatL2.search does: the columns
+    past the database hold id -1 and distance FLT_MAX (faiss's CMax heap neutral; faiss is not
+    importable here, so the pad value is parity-unpinned)."""
     import torch
 
     from haag_vq import _arrays, _native
 
     n = vectors.shape[0]
     nq = queries.shape[0]
-    k = min(int(k), n)
-    ids_out = np.empty((nq, k), dtype=np.int64)
-    dist_out = np.empty((nq, k), dtype=np.float32)
+    k_req = int(k)
+    ids_out = np.full((nq, k_req), -1, dtype=np.int64)
+    dist_out = np.full((nq, k_req), np.finfo(np.float32).max, dtype=np.float32)
+    k = min(k_req, n)
     if nq == 0 or k == 0:
         return ids_out, dist_out
     Qd = _arrays.to_device(np.array(queries, dtype=np.float32, copy=True))
@@ -59,8 +64,8 @@ def exact_knn_l2(vectors: np.ndarray, queries: np.ndarray, k: int, batch_size: i
         d, i = parts_d[0], parts_i[0]
     else:
         d, i = _native.topk_merge(torch.stack(parts_d).contiguous(), torch.stack(parts_i).contiguous(), k)
-    ids_out[:] = _arrays.to_host(i).view(np.uint32).astype(np.int64)
-    dist_out[:] = _arrays.to_host(d)
+    ids_out[:, :k] = _arrays.to_host(i).view(np.uint32).astype(np.int64)
+    dist_out[:, :k] = _arrays.to_host(d)
     return ids_out, dist_out
 
 

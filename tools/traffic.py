@@ -7,15 +7,14 @@ Per dispatch: FETCH_SIZE x 2 (gfx950: FETCH_SIZE counts half the bytes of a wide
 read, MI355X_MICROARCH.md HBM section) + WRITE_SIZE, both in KiB; the mean over the last_n
 dispatches of each kernel, summed over the kernels of a workload.
 """
-import csv
-import glob
 import json
 import sys
-from collections import defaultdict
 from pathlib import Path
 
 ROOT = Path(__file__).resolve().parent.parent
 sys.path.insert(0, str(ROOT / "vector-quantization_amd"))
+sys.path.insert(0, str(ROOT / "tools"))
+from pmc_select import select  # noqa: E402
 
 # workload -> kernel-name substrings (template arguments select the shape)
 WORKLOADS = {
@@ -31,18 +30,14 @@ WORKLOADS = {
 
 
 def per_launch(root, sub, last_n):
-    vals = defaultdict(list)
-    for f in sorted(glob.glob(f"{root}/p*/**/*counter_collection.csv", recursive=True)):
-        rows = [r for r in csv.DictReader(open(f)) if sub in r["Kernel_Name"]]
-        ids = sorted({int(r["Dispatch_Id"]) for r in rows})[-last_n:]
-        for r in rows:
-            if int(r["Dispatch_Id"]) in ids and r["Counter_Name"] in ("FETCH_SIZE", "WRITE_SIZE"):
-                vals[r["Counter_Name"]].append(float(r["Counter_Value"]))
-    if not vals["FETCH_SIZE"]:
-        return None
+    """Mean HBM bytes of the selected dispatches (tools/pmc_select.py: the kernel's largest grid,
+    last_n of each pass; refuses a selection that mixes grid sizes) and that grid size."""
+    vals, _, grid = select(root, sub, last_n)
+    if not vals.get("FETCH_SIZE"):
+        return None, None
     fetch = sum(vals["FETCH_SIZE"]) / len(vals["FETCH_SIZE"])
     write = sum(vals["WRITE_SIZE"]) / max(1, len(vals["WRITE_SIZE"]))
-    return fetch * 1024 * 2 + write * 1024
+    return fetch * 1024 * 2 + write * 1024, grid
 
 
 def main():
@@ -53,13 +48,16 @@ def main():
     out_path = ROOT / "profiles" / "traffic.json"
     data = {}
     for w, kernels in WORKLOADS.items():
-        parts = {k: per_launch(root, k, last_n) for k in kernels}
+        sel = {k: per_launch(root, k, last_n) for k in kernels}
+        parts = {k: v[0] for k, v in sel.items()}
         if all(v is None for v in parts.values()):
             continue
         data[w] = {"bytes_per_launch": sum(v for v in parts.values() if v), "per_kernel": parts,
+                   "grid_sizes": {k: v[1] for k, v in sel.items()},
                    "kernel_source_hash": _native.kernel_source_hash(),
                    "source": f"{root}: rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE (separate passes), FETCH x2 "
-                             f"(gfx950 correction), mean of the last {last_n} dispatches per kernel"}
+                             f"(gfx950 correction), mean of the last {last_n} dispatches per kernel "
+                             f"among those with its largest grid (tools/pmc_select.py)"}
     out_path.write_text(json.dumps(data, indent=1) + "\n")
     print(json.dumps(data, indent=1))
 

@@ -117,6 +117,13 @@ int mivq_opq_prepare(const float* A, int32_t d, int32_t transpose, void* prep, v
 size_t mivq_opq_rotate_workspace_bytes(int64_t n, int32_t d);
 int mivq_opq_rotate_prepared(const float* x, int64_t n, int32_t d, const void* prep, void* workspace,
                              size_t workspace_bytes, float* y, void* stream);
+/* Training: G = X^T Y in fp64 (d, d) row-major for the OPQ orthogonal-Procrustes update
+ * (OPQMatrix::train's X^T Yhat, optimized_product_quantization.py:21-28); x, y: (n, d) f32.
+ * fp64 MFMA, split over rows, the parts added in a fixed order (deterministic).  Workspace:
+ * mivq_opq_gram_workspace_bytes(n, d) bytes, 8-byte aligned. */
+size_t mivq_opq_gram_workspace_bytes(int64_t n, int32_t d);
+int mivq_opq_gram(const float* x, const float* y, int64_t n, int32_t d, void* workspace,
+                  size_t workspace_bytes, double* G, void* stream);
 
 /* ------------------------------------------------------ scalar quantizer
  * Replaces ScalarQuantizer._compress_block / decompress (scalar_quantization.py:52-90)

@@ -126,3 +126,40 @@ def test_opq_codes_are_canonical_encode_of_rotated(dev, oracle):
     _check(Y, X, opq.opq.A.reshape(256, 256).T)
     rec = opq.decompress(codes)
     _check(rec, oracle.pq_decode(codes, C), opq.opq.A.reshape(256, 256))
+
+
+@pytest.mark.parametrize("n,d", [(5000, 200), (70_000, 256), (33, 1536), (0, 64)])
+def test_opq_gram_matches_fp64(dev, n, d):
+    """mivq_opq_gram: G = X^T Y in fp64 (split over rows, parts added in order) vs numpy fp64;
+    every product is exact, only the summation order differs."""
+    from haag_vq import _native
+
+    rng = np.random.default_rng(n + d)
+    X = rng.standard_normal((n, d)).astype(np.float32)
+    Y = (rng.standard_normal((n, d)) * rng.uniform(0.01, 100, d)).astype(np.float32)
+    G = _native.opq_gram(_t(X, dev), _t(Y, dev)).cpu().numpy()
+    ref = X.astype(np.float64).T @ Y.astype(np.float64)
+    bound = 1e-13 * (np.abs(X).astype(np.float64).T @ np.abs(Y).astype(np.float64)) + 1e-300
+    assert np.all(np.abs(G - ref) <= bound * max(1, n) ** 0.5 + 0)
+
+
+def test_polar_factor_newton_schulz(dev):
+    """polar_factor: the orthogonal polar factor U V^T of an ill-conditioned G (kappa ~ 1e4)
+    from the Newton-Schulz iteration on the fp64 MFMA GEMM, vs numpy's SVD; a rank-deficient
+    G takes the SVD fallback and still returns an orthogonal matrix."""
+    from haag_vq.methods.optimized_product_quantization import polar_factor
+
+    rng = np.random.default_rng(8)
+    d = 300
+    U, _ = np.linalg.qr(rng.standard_normal((d, d)))
+    V, _ = np.linalg.qr(rng.standard_normal((d, d)))
+    S = np.logspace(0, -4, d)
+    G = (U * S) @ V.T
+    Q = polar_factor(_t(G, dev)).cpu().numpy()
+    np.testing.assert_allclose(Q, U @ V.T, atol=1e-9)
+    np.testing.assert_allclose(Q.T @ Q, np.eye(d), atol=1e-12)
+    S[-3:] = 0.0  # rank deficient: Newton-Schulz keeps the zero singular values -> fallback
+    Gd = (U * S) @ V.T
+    Qd = polar_factor(_t(Gd, dev)).cpu().numpy()
+    np.testing.assert_allclose(Qd.T @ Qd, np.eye(d), atol=1e-10)
+    np.testing.assert_allclose(Qd @ (Qd.T @ Gd), Gd, atol=1e-10)

@@ -387,6 +387,290 @@ __global__ __launch_bounds__(WR * WC * 64) void opq_split_gemm_kernel(const floa
     store_tile<RB, CB>(acc, smem, w, l, r0 + wr * RB * 32, c0 + wc * CB * 32, n, d, rs, hdr[1], y);
 }
 
+// ------------------------------------------------------------ split-f16, pipelined (round 4)
+// The same arithmetic as opq_split_gemm_kernel (x_hi b_hi + x_hi b_lo + x_lo b_hi, f16 MFMAs,
+// fp32 accumulators) on a 256 x 256 tile with FOUR waves of 128 x 128 (4 x 4 blocks of
+// v_mfma_f32_32x32x16_f16 each, accumulators in AGPRs, one wave per SIMD, up to 512 registers):
+// * K steps of 16 (one MFMA K-slice): a stage is 16 KiB of x and 16 KiB of the B image, four
+//   16-B loads of each per thread, so two register sets (global -> register staging two steps
+//   ahead) fit next to the fragments; range-checked buffer loads (no lane branches);
+// * the split + LDS store of step s + 1 is interleaved with the 48 MFMAs of step s
+//   (sched_group_barrier), so its VALU and DS-write work issues in the MFMAs' shadow instead of
+//   in a phase of its own -- round 3's 8-wave kernel runs load / MFMA / split-and-store / barrier
+//   in lock step with the MFMA pipe about half busy;
+// * one barrier per K step with only lgkmcnt(0) before it: the next steps' global loads stay in
+//   flight across it (no vmcnt(0) in the loop).
+// LDS rows of 16 halves + 16 B pad (48 B): the fragment reads of a 16-lane group hit 16 distinct
+// 4-bank groups.  No LDS DMA.
+constexpr int PP_T = 256, PP_NT = 256, PP_K = 16, PP_U = 4;
+constexpr int PP_PITCH = PP_K * 2 + 16;       // bytes per LDS row
+constexpr int PP_PL = PP_T * PP_PITCH;        // one plane (x hi, x lo, B hi or B lo) of a stage
+constexpr int PP_BUF = 4 * PP_PL;             // 48 KiB per stage
+
+typedef unsigned int u32x4v __attribute__((ext_vector_type(4)));
+typedef _Float16 half2v __attribute__((ext_vector_type(2)));
+typedef float float2v __attribute__((ext_vector_type(2)));
+
+// v = s * (a, b): (hi, lo) f16 pairs packed in two dwords, hi = f16(v), lo = f16(v - hi)
+__device__ __forceinline__ void split_pair(float a, float b, float s, uint32_t& hi, uint32_t& lo) {
+    const float va = a * s, vb = b * s;
+    const half2v h = __builtin_convertvector((float2v){va, vb}, half2v);
+    const float2v hf = __builtin_convertvector(h, float2v);
+    const half2v lw = __builtin_convertvector((float2v){va - hf.x, vb - hf.y}, half2v);
+    hi = __builtin_bit_cast(uint32_t, h);
+    lo = __builtin_bit_cast(uint32_t, lw);
+}
+
+__global__ __launch_bounds__(PP_NT, 1) void opq_pp_gemm_kernel(const float* __restrict__ x, int64_t n, int d,
+                                                                 const float* __restrict__ rs,
+                                                                 const _Float16* __restrict__ bimg,
+                                                                 const float* __restrict__ hdr, float* __restrict__ y,
+                                                                 int64_t ctiles) {
+    // two LDS objects, one per stage: the compiler can then prove that the stores into the next
+    // stage never alias the fragment reads of the current one and interleave them with the MFMAs
+    __shared__ __attribute__((aligned(16))) unsigned char st0[PP_BUF];
+    __shared__ __attribute__((aligned(16))) unsigned char st1[PP_BUF];
+    const int tid = threadIdx.x, l = tid & 63;
+    const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int wr = w >> 1, wc = w & 1;
+    const int64_t t = xcd_tile(blockIdx.x, gridDim.x);
+    const int64_t r0 = (t / ctiles) * PP_T;
+    const int c0 = (int)(t % ctiles) * PP_T;
+    const int64_t dd = (int64_t)d * d;
+    const int nrows = (int)min<int64_t>(PP_T, n - r0);
+
+    // x: load u reads row xr0 + 64 u, dims k0 + xk .. +3; B: load u reads plane u >> 1, column
+    // bc0 + 128 (u & 1), dims k0 + bk .. +7
+    const int xr0 = tid >> 2, xk = 4 * (tid & 3);
+    const int bc0 = tid >> 1, bk = 8 * (tid & 1);
+    const __amdgpu_buffer_rsrc_t xsrc =
+        __builtin_amdgcn_make_buffer_rsrc((void*)(x + r0 * d), 0, (int)((int64_t)nrows * d * 4), 0x00020000);
+    const __amdgpu_buffer_rsrc_t bsrc =
+        __builtin_amdgcn_make_buffer_rsrc((void*)bimg, 0, (int)(2 * dd * 2), 0x00020000);
+    float sx[PP_U];
+    int xo[PP_U], bo[PP_U];
+#pragma unroll
+    for (int u = 0; u < PP_U; ++u) {
+        const int rr = xr0 + 64 * u;
+        sx[u] = rr < nrows ? rs[r0 + rr] : 0.0f;
+        xo[u] = (rr * d + xk) * 4;
+        const int gc = c0 + bc0 + 128 * (u & 1);
+        bo[u] = gc < d ? (int)(((u >> 1) * dd + (int64_t)gc * d + bk) * 2) : (int)0x80000000u;
+    }
+    u32x4v xv[2][PP_U], bv[2][PP_U];
+    auto gload = [&](int set, int k0) __attribute__((always_inline)) {
+        // the step's k0 rides in soffset (SALU); lanes whose dims pass d read past the range
+        const bool xin = k0 + xk < d, bin = k0 + bk < d;
+#pragma unroll
+        for (int u = 0; u < PP_U; ++u) {
+            xv[set][u] = __builtin_amdgcn_raw_buffer_load_b128(xsrc, xin ? xo[u] : (int)0x80000000u, k0 * 4, 0);
+            bv[set][u] = __builtin_amdgcn_raw_buffer_load_b128(bsrc, bin ? bo[u] : (int)0x80000000u, k0 * 2, 0);
+        }
+    };
+    auto sstore = [&](int set, unsigned char* buf) __attribute__((always_inline)) {
+#pragma unroll
+        for (int u = 0; u < PP_U; ++u) {
+            const u32x4v v = xv[set][u];
+            uint32_t h0, l0, h1, l1;
+            split_pair(__uint_as_float(v[0]), __uint_as_float(v[1]), sx[u], h0, l0);
+            split_pair(__uint_as_float(v[2]), __uint_as_float(v[3]), sx[u], h1, l1);
+            const int off = (xr0 + 64 * u) * PP_PITCH + 2 * xk;
+            *reinterpret_cast<uint2*>(buf + off) = make_uint2(h0, h1);
+            *reinterpret_cast<uint2*>(buf + PP_PL + off) = make_uint2(l0, l1);
+            *reinterpret_cast<u32x4v*>(buf + (2 + (u >> 1)) * PP_PL + (bc0 + 128 * (u & 1)) * PP_PITCH + 2 * bk) =
+                bv[set][u];
+        }
+    };
+
+    floatx16 acc[4][4];
+#pragma unroll
+    for (int a = 0; a < 4; ++a)
+#pragma unroll
+        for (int b = 0; b < 4; ++b)
+#pragma unroll
+            for (int e = 0; e < 16; ++e) acc[a][b][e] = 0.0f;
+
+    const int fr = l & 31, fk = 16 * (l >> 5);
+    // the 48 MFMAs of one K step from stage buffer `cur`: the A fragments (x hi / lo of the
+    // wave's 4 row blocks) stay live, the B fragments are read per column block
+    auto mfma_step = [&](const unsigned char* cur) __attribute__((always_inline)) {
+        half8 ah[4], al[4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const int ar = (wr * 128 + i * 32 + fr) * PP_PITCH + fk;
+            ah[i] = *reinterpret_cast<const half8*>(cur + ar);
+            al[i] = *reinterpret_cast<const half8*>(cur + PP_PL + ar);
+        }
+#pragma unroll
+        for (int b = 0; b < 4; ++b) {
+            const int bc = (wc * 128 + b * 32 + fr) * PP_PITCH + fk;
+            const half8 bh = *reinterpret_cast<const half8*>(cur + 2 * PP_PL + bc);
+            const half8 bl = *reinterpret_cast<const half8*>(cur + 3 * PP_PL + bc);
+            // small terms first; the three MFMAs of one accumulator four apart
+#pragma unroll
+            for (int a = 0; a < 4; ++a) acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x16_f16(al[a], bh, acc[a][b], 0, 0, 0);
+#pragma unroll
+            for (int a = 0; a < 4; ++a) acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[a], bl, acc[a][b], 0, 0, 0);
+#pragma unroll
+            for (int a = 0; a < 4; ++a) acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[a], bh, acc[a][b], 0, 0, 0);
+        }
+    };
+    auto barrier = []() __attribute__((always_inline)) {
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();
+        asm volatile("" ::: "memory");
+    };
+    // one K step: MFMAs of stage s (buffer s & 1) with the store of stage s + 1 (register set
+    // (s + 1) & 1 -> buffer (s + 1) & 1) between them; the loads of stage s + 2 into set s & 1
+    // (stored one step ago) go out first
+    auto step = [&](int s, int set, bool load2, bool store1) __attribute__((always_inline)) {
+        unsigned char* cur = set ? st1 : st0;
+        unsigned char* nxt = set ? st0 : st1;
+        if (load2) gload(set, (s + 2) * PP_K);
+        __builtin_amdgcn_sched_barrier(0);  // the loads go out first, whatever the scheduler prefers
+        mfma_step(cur);
+        if (store1) sstore(set ^ 1, nxt);
+        // the A fragments first, then per 4 MFMAs: a B fragment read, 6 split ops, 1 LDS store
+        __builtin_amdgcn_sched_group_barrier(0x100, 8, 0);
+#pragma unroll
+        for (int i = 0; i < 12; ++i) {
+            __builtin_amdgcn_sched_group_barrier(0x8, 4, 0);
+            __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+            __builtin_amdgcn_sched_group_barrier(0x2, 6, 0);
+            __builtin_amdgcn_sched_group_barrier(0x200, 1, 0);
+        }
+        __builtin_amdgcn_sched_barrier(0);
+        barrier();
+    };
+
+    const int nsteps = (d + PP_K - 1) / PP_K;
+    gload(0, 0);
+    if (nsteps > 1) gload(1, PP_K);
+    sstore(0, st0);
+    barrier();
+    int s = 0;
+    for (; s + 3 < nsteps; s += 2) {  // steady state: both sets in use, no conditions
+        step(s, 0, true, true);
+        step(s + 1, 1, true, true);
+    }
+    // tail (s even here, at most three steps left): constant register sets, no dynamic indexing
+    if (s < nsteps) step(s, 0, s + 2 < nsteps, s + 1 < nsteps);
+    if (s + 1 < nsteps) step(s + 1, 1, s + 3 < nsteps, s + 2 < nsteps);
+    if (s + 2 < nsteps) step(s + 2, 0, false, s + 3 < nsteps);
+    // epilogue: each wave's 16 KiB slice, waves 0-1 in stage 0's buffer, 2-3 in stage 1's (every
+    // wave passed the last barrier, so both buffers are dead)
+    store_tile<4, 4>(acc, w < 2 ? st0 : st1, w & 1, l, r0 + wr * 128, c0 + wc * 128, n, d, rs, hdr[1], y);
+}
+
+// ------------------------------------------------------------ Procrustes Gram matrix (training)
+// G = X^T Y in fp64 for the OPQ update (faiss OPQMatrix::train's X^T Yhat before its SVD,
+// /root/reference/src/haag_vq/methods/optimized_product_quantization.py:21-28): X, Y (n, d) f32
+// rows, each product exact in fp64 (24 + 24 bits), sums in fp64 on v_mfma_f64_16x16x4_f64.
+// Split K: workgroup (tile, s) sums rows [s R, (s + 1) R) of a 128 x 128 tile of G into
+// part[s]; opq_gram_reduce_kernel adds the parts in s order (deterministic).  4 waves of 64 x 64
+// (4 x 4 blocks); f64 operand map as erq_rotate_kernel: A[l & 15][l >> 4], B[l >> 4][l & 15],
+// D column l & 15, rows (l >> 4) + 4 g.
+constexpr int GR_T = 128, GR_K = 16, GR_P = GR_T + 2;  // LDS rows of 130 doubles: [k][i]
+typedef double f64x4g __attribute__((ext_vector_type(4)));
+
+__global__ __launch_bounds__(256) void opq_gram_kernel(const float* __restrict__ X, const float* __restrict__ Y,
+                                                         int64_t n, int d, int64_t rows_per_split, int ctiles,
+                                                         double* __restrict__ part) {
+    __shared__ double As[2][GR_K * GR_P];
+    __shared__ double Bs[2][GR_K * GR_P];
+    const int tid = threadIdx.x, l = tid & 63, w = tid >> 6;
+    const int wr = w >> 1, wc = w & 1;
+    const int tile = blockIdx.x, sp = blockIdx.y;
+    const int i0 = (tile / ctiles) * GR_T, j0 = (tile % ctiles) * GR_T;
+    const int64_t ra = (int64_t)sp * rows_per_split;
+    const int64_t rb = min(n, ra + rows_per_split);
+    f64x4g acc[4][4];
+#pragma unroll
+    for (int a = 0; a < 4; ++a)
+#pragma unroll
+        for (int b = 0; b < 4; ++b) acc[a][b] = (f64x4g){0.0, 0.0, 0.0, 0.0};
+    // staging: thread t loads rows k = t >> 4 of the 16-row step, columns 8 (t & 15) .. +7 of the
+    // tile (two float4 of X, two of Y); out-of-range rows / columns read as 0
+    const int kr = tid >> 4, cc = 8 * (tid & 15);
+    float xa[8], yb[8];
+    auto gload = [&](int64_t r) __attribute__((always_inline)) {
+        const int64_t row = r + kr;
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+            const int ci = i0 + cc + u, cj = j0 + cc + u;
+            xa[u] = (row < rb && ci < d) ? X[row * d + ci] : 0.0f;
+            yb[u] = (row < rb && cj < d) ? Y[row * d + cj] : 0.0f;
+        }
+    };
+    auto sstore = [&](int st) __attribute__((always_inline)) {
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+            As[st][kr * GR_P + cc + u] = (double)xa[u];
+            Bs[st][kr * GR_P + cc + u] = (double)yb[u];
+        }
+    };
+    const int64_t nk = (rb - ra + GR_K - 1) / GR_K;
+    if (nk <= 0) {
+#pragma unroll
+        for (int a = 0; a < 4; ++a)
+#pragma unroll
+            for (int b = 0; b < 4; ++b)
+#pragma unroll
+                for (int g = 0; g < 4; ++g) {
+                    const int i = i0 + wr * 64 + a * 16 + (l >> 4) + 4 * g, j = j0 + wc * 64 + b * 16 + (l & 15);
+                    if (i < d && j < d) part[((int64_t)sp * d + i) * d + j] = 0.0;
+                }
+        return;
+    }
+    gload(ra);
+    sstore(0);
+    __syncthreads();
+    const int fi = l & 15, fk = l >> 4;
+    for (int64_t ks = 0; ks < nk; ++ks) {
+        const int st = (int)(ks & 1);
+        if (ks + 1 < nk) gload(ra + (ks + 1) * GR_K);
+#pragma unroll
+        for (int k4 = 0; k4 < GR_K; k4 += 4) {
+            double af[4], bf[4];
+#pragma unroll
+            for (int a = 0; a < 4; ++a) af[a] = As[st][(k4 + fk) * GR_P + wr * 64 + a * 16 + fi];
+#pragma unroll
+            for (int b = 0; b < 4; ++b) bf[b] = Bs[st][(k4 + fk) * GR_P + wc * 64 + b * 16 + fi];
+#pragma unroll
+            for (int a = 0; a < 4; ++a)
+#pragma unroll
+                for (int b = 0; b < 4; ++b) acc[a][b] = __builtin_amdgcn_mfma_f64_16x16x4f64(af[a], bf[b], acc[a][b], 0, 0, 0);
+        }
+        if (ks + 1 < nk) sstore(st ^ 1);
+        __syncthreads();
+    }
+#pragma unroll
+    for (int a = 0; a < 4; ++a)
+#pragma unroll
+        for (int b = 0; b < 4; ++b)
+#pragma unroll
+            for (int g = 0; g < 4; ++g) {
+                const int i = i0 + wr * 64 + a * 16 + fk + 4 * g, j = j0 + wc * 64 + b * 16 + fi;
+                if (i < d && j < d) part[((int64_t)sp * d + i) * d + j] = acc[a][b][g];
+            }
+}
+
+__global__ __launch_bounds__(256) void opq_gram_reduce_kernel(const double* __restrict__ part, int splits, int64_t dd,
+                                                                double* __restrict__ G) {
+    const int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (e >= dd) return;
+    double s = part[e];
+    for (int p = 1; p < splits; ++p) s += part[(int64_t)p * dd + e];
+    G[e] = s;
+}
+
+int gram_splits(int64_t n, int d) {
+    const int64_t tiles = ceil_div(d, GR_T) * ceil_div(d, GR_T);
+    int64_t s = std::max<int64_t>(1, ceil_div(512, tiles));          // >= 2 rounds of workgroups
+    s = std::min<int64_t>(s, std::max<int64_t>(1, ceil_div(n, 4 * GR_K)));  // >= 4 K steps each
+    return (int)std::min<int64_t>(s, 64);
+}
+
 template <class T, int WR, int WC, int RB, int CB>
 int launch_split(const float* x, int64_t n, int d, const float* rs, const _Float16* bimg, const float* hdr, float* y,
                  hipStream_t st) {
@@ -399,6 +683,15 @@ int launch_split(const float* x, int64_t n, int d, const float* rs, const _Float
                  (long long)n);
     hipLaunchKernelGGL(kern, dim3((unsigned)tiles), dim3(T::NT), T::SMEM, st, x, n, d, rs, bimg, hdr, y, ct);
     return check_launch("opq_split_gemm");
+}
+
+int launch_pp(const float* x, int64_t n, int d, const float* rs, const _Float16* bimg, const float* hdr, float* y,
+              hipStream_t st) {
+    const int64_t ct = ceil_div(d, PP_T), tiles = ceil_div(n, PP_T) * ct;
+    MIVQ_REQUIRE(tiles < ((int64_t)1 << 31), MIVQ_ERR_UNSUPPORTED, "opq_rotate_prepared: n=%lld too large for one call",
+                 (long long)n);
+    hipLaunchKernelGGL(opq_pp_gemm_kernel, dim3((unsigned)tiles), dim3(PP_NT), 0, st, x, n, d, rs, bimg, hdr, y, ct);
+    return check_launch("opq_pp_gemm");
 }
 
 size_t prep_bytes(int32_t d) { return 256 + (size_t)2 * d * d * sizeof(_Float16); }
@@ -475,7 +768,13 @@ extern "C" int mivq_opq_rotate_prepared(const float* x, int64_t n, int32_t d, co
 #ifndef MIVQ_OPQ_TILE4
 #define MIVQ_OPQ_TILE4 0
 #endif
-        if (d >= 256 && cn >= 256)
+#ifndef MIVQ_OPQ_PP
+#define MIVQ_OPQ_PP 1
+#endif
+        // (the pipelined kernel's buffer offsets into the B image are 32-bit: 4 d^2 < 2^31)
+        if (d >= 256 && cn >= 256 && MIVQ_OPQ_PP && (int64_t)4 * d * d < ((int64_t)1 << 31))
+            rc = launch_pp(xc, cn, d, rs + c0, bimg, hdr, yc, st);
+        else if (d >= 256 && cn >= 256)
             rc = MIVQ_OPQ_TILE4 ? launch_split<TileW, 2, 2, 4, 4>(xc, cn, d, rs + c0, bimg, hdr, yc, st)
                                 : launch_split<TileL, 4, 2, 2, 4>(xc, cn, d, rs + c0, bimg, hdr, yc, st);
         else
@@ -483,4 +782,34 @@ extern "C" int mivq_opq_rotate_prepared(const float* x, int64_t n, int32_t d, co
         if (rc) return rc;
     }
     return MIVQ_OK;
+}
+
+extern "C" size_t mivq_opq_gram_workspace_bytes(int64_t n, int32_t d) {
+    if (n <= 0 || d <= 0) return 0;
+    return (size_t)gram_splits(n, d) * (size_t)d * d * sizeof(double);
+}
+
+extern "C" int mivq_opq_gram(const float* x, const float* y, int64_t n, int32_t d, void* workspace,
+                             size_t workspace_bytes, double* G, void* stream) {
+    MIVQ_REQUIRE(n >= 0 && d > 0, MIVQ_ERR_INVALID, "opq_gram: bad sizes n=%lld d=%d", (long long)n, d);
+    MIVQ_REQUIRE(x && y && G, MIVQ_ERR_INVALID, "opq_gram: null pointer");
+    hipStream_t st = as_stream(stream);
+    const int64_t dd = (int64_t)d * d;
+    if (n == 0) {
+        hipError_t e = hipMemsetAsync(G, 0, (size_t)dd * sizeof(double), st);
+        return e == hipSuccess ? MIVQ_OK : set_error(MIVQ_ERR_HIP, "opq_gram: %s", hipGetErrorString(e));
+    }
+    const size_t need = mivq_opq_gram_workspace_bytes(n, d);
+    MIVQ_REQUIRE(workspace && workspace_bytes >= need, MIVQ_ERR_WORKSPACE, "opq_gram: workspace %zu < %zu",
+                 workspace_bytes, need);
+    const int splits = gram_splits(n, d);
+    const int ct = (int)ceil_div(d, GR_T);
+    const int64_t rps = ceil_div(n, splits);
+    double* part = static_cast<double*>(workspace);
+    hipLaunchKernelGGL(opq_gram_kernel, dim3((unsigned)(ct * ct), (unsigned)splits), dim3(256), 0, st, x, y, n, d, rps,
+                       ct, part);
+    int rc = check_launch("opq_gram");
+    if (rc) return rc;
+    hipLaunchKernelGGL(opq_gram_reduce_kernel, dim3((unsigned)ceil_div(dd, 256)), dim3(256), 0, st, part, splits, dd, G);
+    return check_launch("opq_gram_reduce");
 }

@@ -157,6 +157,21 @@ __device__ __forceinline__ float dot2_self(uint32_t u, float acc) {
 
 __device__ __forceinline__ uint32_t lds_addr(const void* p) { return (uint32_t)(uintptr_t)p; }
 
+#ifndef MIVQ_CS_PERMLANE
+#define MIVQ_CS_PERMLANE 1
+#endif
+// Lanes 0..31 receive lane l + 32's value (lanes 32..63: their own value back).  The filter's
+// lane pair (l, l + 32) holds one row; only the h = 0 lanes use the merged result, so a
+// v_permlane32_swap (VALU, no LDS round trip) replaces ds_bpermute's __shfl_xor(v, 32).
+__device__ __forceinline__ float upper_half(float v) {
+#if MIVQ_CS_PERMLANE
+    const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+    return __uint_as_float(r[1]);
+#else
+    return __shfl_xor(v, 32);
+#endif
+}
+
 // 8 x reads (stride XS bytes) and the 4 reads of two centroid-pair rows (CS bytes apart),
 // all issued back to back, then one lgkmcnt(0).
 template <int G, int XS, int CS>
@@ -440,7 +455,7 @@ __global__ __launch_bounds__(NW * 64) void pq_encode_cs_kernel(
         }
         if (vb + kDep * kProd < nvb && !((V & 64) && vb >= kProd)) load(vb + kDep * kProd, hh, xr);
         }
-        xx += __shfl_xor(xx, 32);
+        xx += upper_half(xx);  // lanes 0..31: the row norm over both halves
 
         // Candidates: the 16 packed scores of centroid block cb in this lane form a group; each
         // group keeps its top-2 (g1, g2: pack, then max3 + med3 + max per two scores), and (t1, t2, t3) is the
@@ -520,7 +535,7 @@ __global__ __launch_bounds__(NW * 64) void pq_encode_cs_kernel(
         t2 = __uint_as_float(__float_as_uint(t2) | hbit);
         t3 = __uint_as_float(__float_as_uint(t3) | hbit);
         {
-            const float p1 = __shfl_xor(t1, 32), p2 = __shfl_xor(t2, 32), p3 = __shfl_xor(t3, 32);
+            const float p1 = upper_half(t1), p2 = upper_half(t2), p3 = upper_half(t3);
             top3_insert(t1, t2, t3, p1);
             top3_insert(t1, t2, t3, p2);
             top3_insert(t1, t2, t3, p3);
@@ -543,12 +558,27 @@ __global__ __launch_bounds__(NW * 64) void pq_encode_cs_kernel(
             // code when the gap exceeds the pair's own window, else it goes to the list.
             const bool listp = settle_pending();
             append(listp, pend_row, pend_k, 0.0f, 0.0f, mine && ncand >= 3, rowl);
-            pend_row = (mine && ncand == 2) ? rowl : -1;
-            if (pend_row >= 0) {
+            // Every lane loads (a pair-less lane reads the subspace's first entry) and the state is
+            // selected without branches: a load issued under a branch made the compiler wait
+            // vmcnt(0) at the next block's use -- for the next x block's loads too, issued after it.
+#ifndef MIVQ_CS_PD_UNCOND
+#define MIVQ_CS_PD_UNCOND 1
+#endif
+            const bool np = mine && ncand == 2;
+            if (MIVQ_CS_PD_UNCOND) {
+                pend_pd = pdw[((int64_t)m * 256 + (np ? k1 : 0)) * 256 + (np ? k2 : 0)];
+                pend_row = np ? rowl : -1;
                 pend_k = k1 | (k2 << 8);
                 pend_gap = gap;
                 pend_xs = Xs;
-                pend_pd = pdw[((int64_t)m * 256 + k1) * 256 + k2];
+            } else {  // round 3 (profiling builds)
+                pend_row = np ? rowl : -1;
+                if (np) {
+                    pend_k = k1 | (k2 << 8);
+                    pend_gap = gap;
+                    pend_xs = Xs;
+                    pend_pd = pdw[((int64_t)m * 256 + k1) * 256 + k2];
+                }
             }
         } else {
             append(mine && ncand == 2, rowl, k1 | (k2 << 8), gap, Xs, mine && ncand >= 3, rowl);

@@ -58,6 +58,8 @@ SIGNATURES = {
     "mivq_opq_prepare": (_c.c_int, [_vp, _i32, _i32, _vp, _vp]),
     "mivq_opq_rotate_workspace_bytes": (_sz, [_i64, _i32]),
     "mivq_opq_rotate_prepared": (_c.c_int, [_vp, _i64, _i32, _vp, _vp, _sz, _vp, _vp]),
+    "mivq_opq_gram_workspace_bytes": (_sz, [_i64, _i32]),
+    "mivq_opq_gram": (_c.c_int, [_vp, _vp, _i64, _i32, _vp, _sz, _vp, _vp]),
     "mivq_sq_encode_f32": (_c.c_int, [_vp, _i64, _i32, _vp, _vp, _i32, _vp, _vp]),
     "mivq_sq_encode_f64": (_c.c_int, [_vp, _i64, _i32, _vp, _vp, _i32, _vp, _vp]),
     "mivq_sq_decode_f32": (_c.c_int, [_vp, _i64, _i32, _vp, _vp, _i32, _vp, _vp]),
@@ -320,6 +322,19 @@ def opq_rotate_prepared(x: torch.Tensor, prep: torch.Tensor, out: Optional[torch
     ws = workspace(load_library().mivq_opq_rotate_workspace_bytes(n, d), x.device)
     _call("mivq_opq_rotate_prepared", _ptr(x), n, d, _ptr(prep), _ptr(ws), ws.numel(), _ptr(out), _stream())
     return out
+
+
+def opq_gram(x: torch.Tensor, y: torch.Tensor) -> torch.Tensor:
+    """G = x^T y in fp64 (d, d) on the library's fp64 MFMA kernel (OPQ Procrustes step)."""
+    _check(x, "x", torch.float32, 2)
+    _check(y, "y", torch.float32, 2)
+    if x.shape != y.shape:
+        raise ValueError(f"opq_gram: x {tuple(x.shape)} and y {tuple(y.shape)} differ")
+    n, d = x.shape
+    G = torch.empty((d, d), dtype=torch.float64, device=x.device)
+    ws = workspace(load_library().mivq_opq_gram_workspace_bytes(n, d), x.device)
+    _call("mivq_opq_gram", _ptr(x), _ptr(y), n, d, _ptr(ws), ws.numel(), _ptr(G), _stream())
+    return G
 
 
 # ----------------------------------------------------------------- SQ

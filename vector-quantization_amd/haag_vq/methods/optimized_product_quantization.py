@@ -14,8 +14,10 @@ Drop-in for the reference's ``OptimizedProductQuantizer``
 Hot path on device: the rotation is ``mivq_opq_rotate_prepared`` (hand-written split-f16
 MFMA GEMM with fp32 accuracy; the f16 hi / lo image of A is prepared once per matrix and
 direction), encode / decode are the PQ kernels.  ``mivq_opq_rotate`` (plain fp32 MFMA, no
-preparation) serves dimensions that are not multiples of 8.  The Procrustes step of training (a D x D product and SVD) uses
-the vendor libraries through torch — it is training, not the encode path.
+preparation) serves dimensions that are not multiples of 8.  The Procrustes step of training
+runs on repo kernels too (round 4): the fp64 Gram matrix X^T Yhat on ``mivq_opq_gram`` and the
+polar factor of it by a Newton-Schulz iteration on the fp64 MFMA GEMM (``polar_factor``), with
+torch's SVD only as the fallback for a matrix the iteration cannot orthogonalise.
 """
 
 from __future__ import annotations
@@ -80,6 +82,48 @@ class OPQHandle:
         return self._run(y, True)
 
 
+def _mm(a: torch.Tensor, b: torch.Tensor) -> torch.Tensor:
+    """a . b for square fp64 device matrices on the library's fp64 MFMA GEMM."""
+    return _native.extrabitq_rotate(a.contiguous(), b.contiguous(), False)
+
+
+def polar_factor(G: torch.Tensor, tol: float = 1e-13, max_iter: int = 60) -> torch.Tensor:
+    """The orthogonal polar factor Q = U V^T of a square fp64 matrix G = U S V^T (what
+    faiss OPQMatrix::train takes from its SVD), by the Newton-Schulz iteration
+    Q <- Q (3 I - Q^T Q) / 2 on the fp64 MFMA GEMM (erq_rotate_kernel) instead of rocsolver's
+    SVD.  Start: G scaled by 1.1 x a power-iteration estimate of its largest singular value
+    (the iteration converges for singular values in (0, sqrt(3))); it doubles the digits once
+    every singular value is near 1, and stops at ||Q^T Q - I||_F < tol sqrt(d) or once that
+    error stalls at the fp64 rounding floor of the GEMMs.  A G the iteration cannot orthogonalise
+    (rank deficient, or not converged within max_iter: condition numbers far beyond 1e8) falls
+    back to the SVD."""
+    d = G.shape[0]
+    I = torch.eye(d, dtype=torch.float64, device=G.device)
+    v = torch.ones((d,), dtype=torch.float64, device=G.device) / d ** 0.5
+    GtG = _mm(G.T, G)
+    smax2 = 0.0
+    for _ in range(12):  # power iteration on G^T G (element-wise + row sums: no BLAS call)
+        w = (GtG * v.view(1, d)).sum(dim=1)
+        smax2 = float(w.norm())
+        if not smax2 > 0.0:
+            break
+        v = w / smax2
+    if smax2 > 0.0 and smax2 < float("inf"):
+        Q = G / (1.1 * smax2 ** 0.5)
+        prev = float("inf")
+        for _ in range(max_iter):
+            T = _mm(Q.T, Q)
+            err = float((T - I).norm())
+            if err < tol * d ** 0.5 or (err < 1e-8 and err > 0.25 * prev):
+                return Q  # converged (quadratic phase stalled: the rounding floor)
+            if not err < 1e3:  # diverging or non-finite
+                break
+            prev = err
+            Q = 1.5 * Q - 0.5 * _mm(Q, T)
+    U, _, Vh = torch.linalg.svd(G)
+    return U @ Vh
+
+
 class OptimizedProductQuantizer(BaseQuantizer):
     def __init__(self, M: int, B: int = 8):
         """OPQ (Ge et al., TPAMI 2013).  M sub-quantizers of 2**B centroids."""
@@ -120,10 +164,10 @@ class OptimizedProductQuantizer(BaseQuantizer):
                      seed=self.seed, max_points_per_centroid=1000, init=C)
         prep = _native.pq_prepare(C, self.B)
         Yhat = _native.pq_decode(_native.pq_encode(Y, C, prep, self.B), C, self.B)
-        # orthogonal Procrustes: argmin_R ||X R^T - Yhat||  ->  R = V U^T, X^T Yhat = U S V^T
-        G = (X.double().T @ Yhat.double())
-        U, _, Vh = torch.linalg.svd(G)
-        return (Vh.T @ U.T).float().contiguous(), C, Y, Yhat
+        # orthogonal Procrustes: argmin_R ||X R^T - Yhat||  ->  R = V U^T = Q^T with
+        # X^T Yhat = U S V^T and Q = U V^T its orthogonal polar factor
+        G = _native.opq_gram(X, Yhat)
+        return polar_factor(G).T.float().contiguous(), C, Y, Yhat
 
     def fit(self, X) -> None:
         Xd = _arrays.to_device(X, torch.float32)

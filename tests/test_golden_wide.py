@@ -76,6 +76,29 @@ def _erq_unpack(cb, D, nb):
     return (bits.astype(np.int64) << np.arange(nb - 1, -1, -1)).sum(-1)
 
 
+def _check_P(erqw, tag, P):
+    """The regenerated rotation equals the fixture's to rounding (numpy's QR is bit-identical
+    only on the same CPU: the sha is compared where it can be, the samples everywhere)."""
+    np.testing.assert_allclose(P[:8], erqw[f"{tag}_P_head"], rtol=0, atol=1e-13)
+    np.testing.assert_allclose(P.sum(axis=0), erqw[f"{tag}_P_colsum"], rtol=0, atol=1e-12)
+    return _sha(P) == str(erqw[f"{tag}_P_sha"])
+
+
+def _assert_ties_only(got, ref, X, c, P, lv, nbits, max_frac=1e-3):
+    """Index mismatches only where s sits on a level midpoint (fp64 rounding), one level apart."""
+    N, D = X.shape
+    gi, ri = _erq_unpack(got, D, nbits), _erq_unpack(ref, D, nbits)
+    bad = np.argwhere(gi != ri)
+    r = X.astype(np.float64) - c
+    s = (r / np.maximum(np.linalg.norm(r, axis=1), 1e-12)[:, None] @ P) * np.sqrt(D)
+    mids = 0.5 * (lv[:-1] + lv[1:])
+    for i, j in bad:
+        assert np.min(np.abs(mids - s[i, j])) <= 1e-12 * max(1.0, abs(s[i, j])), (i, j)
+        assert abs(int(gi[i, j]) - int(ri[i, j])) == 1
+    assert len(bad) <= max_frac * N * D
+    return bad
+
+
 def test_extrabitq_wide_oracle_matches_reference(oracle, erqw, mk):
     X = mk.erq_wide_input()
     assert _sha(X) == str(erqw["X_sha"])
@@ -83,11 +106,14 @@ def test_extrabitq_wide_oracle_matches_reference(oracle, erqw, mk):
         b = int(tag[1:])
         c, P, lv = oracle.extrabitq_fit(X, b)
         np.testing.assert_array_equal(c, erqw[f"{tag}_c"])
-        assert _sha(P) == str(erqw[f"{tag}_P_sha"]), f"{tag}: regenerated rotation differs"
+        same_P = _check_P(erqw, tag, P)
         np.testing.assert_array_equal(lv, erqw[f"{tag}_levels"])
         codes = oracle.extrabitq_encode(X, c, P, lv, b)
-        np.testing.assert_array_equal(codes, erqw[f"{tag}_codes"])
-        np.testing.assert_array_equal(oracle.extrabitq_decode(codes[:32], c, P, lv, b), erqw[f"{tag}_recon_head"])
+        if same_P:  # the generating machine: bit-exact
+            np.testing.assert_array_equal(codes, erqw[f"{tag}_codes"])
+            np.testing.assert_array_equal(oracle.extrabitq_decode(codes[:32], c, P, lv, b), erqw[f"{tag}_recon_head"])
+        else:
+            _assert_ties_only(codes, erqw[f"{tag}_codes"], X, c, P, lv, b)
 
 
 # ------------------------------------------------------------------------------ GPU
@@ -118,20 +144,12 @@ def test_extrabitq_wide_gpu(dev, erqw, mk, oracle, nbits):
     X = mk.erq_wide_input()
     tag = f"b{nbits}"
     c, P, lv = oracle.extrabitq_fit(X, nbits)
-    assert _sha(P) == str(erqw[f"{tag}_P_sha"])
+    _check_P(erqw, tag, P)  # this machine's QR of the seeded matrix = the fixture's to rounding
     t = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(dev)  # noqa: E731
     ref = erqw[f"{tag}_codes"]
     got = _native.extrabitq_encode(t(X), t(c), t(P), t(lv), nbits).cpu().numpy()
     N, D = X.shape
-    gi, ri = _erq_unpack(got, D, nbits), _erq_unpack(ref, D, nbits)
-    bad = np.argwhere(gi != ri)
-    r = X.astype(np.float64) - c
-    s = (r / np.maximum(np.linalg.norm(r, axis=1), 1e-12)[:, None] @ P) * np.sqrt(D)
-    mids = 0.5 * (lv[:-1] + lv[1:])
-    for i, j in bad:
-        assert np.min(np.abs(mids - s[i, j])) <= 1e-12 * max(1.0, abs(s[i, j])), (i, j)
-        assert abs(int(gi[i, j]) - int(ri[i, j])) == 1
-    assert len(bad) <= 1e-3 * N * D
+    bad = _assert_ties_only(got, ref, X, c, P, lv, nbits)
     ib = (D * nbits + 7) // 8
     fg, fr = got[:, ib:].copy().view(np.float32), ref[:, ib:].copy().view(np.float32)
     ok_rows = np.setdiff1d(np.arange(N), bad[:, 0])  # t depends on every index of its row

@@ -768,8 +768,8 @@ extern "C" int mivq_opq_rotate_prepared(const float* x, int64_t n, int32_t d, co
 #ifndef MIVQ_OPQ_TILE4
 #define MIVQ_OPQ_TILE4 0
 #endif
-#ifndef MIVQ_OPQ_PP
-#define MIVQ_OPQ_PP 1
+#ifndef MIVQ_OPQ_PP  // the round-4 4-wave pipelined kernel: measured slower (17.4 vs 16.2 ms), not the default
+#define MIVQ_OPQ_PP 0
 #endif
         // (the pipelined kernel's buffer offsets into the B image are 32-bit: 4 d^2 < 2^31)
         if (d >= 256 && cn >= 256 && MIVQ_OPQ_PP && (int64_t)4 * d * d < ((int64_t)1 << 31))
@@ -792,7 +792,7 @@ extern "C" size_t mivq_opq_gram_workspace_bytes(int64_t n, int32_t d) {
 extern "C" int mivq_opq_gram(const float* x, const float* y, int64_t n, int32_t d, void* workspace,
                              size_t workspace_bytes, double* G, void* stream) {
     MIVQ_REQUIRE(n >= 0 && d > 0, MIVQ_ERR_INVALID, "opq_gram: bad sizes n=%lld d=%d", (long long)n, d);
-    MIVQ_REQUIRE(x && y && G, MIVQ_ERR_INVALID, "opq_gram: null pointer");
+    MIVQ_REQUIRE(G && (n == 0 || (x && y)), MIVQ_ERR_INVALID, "opq_gram: null pointer");
     hipStream_t st = as_stream(stream);
     const int64_t dd = (int64_t)d * d;
     if (n == 0) {

@@ -73,13 +73,19 @@ typedef float f32x4 __attribute__((ext_vector_type(4)));
 #define MIVQ_GC_LIST_NC 4
 #endif
 constexpr int kWaves = MIVQ_CS_WAVES;  // 768 threads, 3 waves per SIMD (profiling builds may override)
-constexpr int kDepth = 1;   // x blocks in flight per wave
+
 // Wide subspaces (dsub 97..192, KS 7..12): the f16 image alone takes up to 96 KiB of LDS, so
 // the filter runs 4 waves (one per SIMD, up to 512 registers) with two blocks in flight each.
 constexpr int kWideWaves = 4;
 constexpr int cs_waves(int KS) { return KS <= 6 ? kWaves : kWideWaves; }
 constexpr int kRsrcWord3 = 0x00020000;  // gfx9 buffer resource: 32-bit data format
-constexpr int kXAux = 2;  // x stream cache policy: nt (read once)
+#ifndef MIVQ_CS_XAUX
+#define MIVQ_CS_XAUX 2
+#endif
+constexpr int kXAux = MIVQ_CS_XAUX;  // x stream cache policy: nt (read once)
+#ifndef MIVQ_CS_PRIO  // profiling: s_setprio 1 around each centroid block's MFMAs
+#define MIVQ_CS_PRIO 0
+#endif
 
 // Keeps the three largest of a stream of packed scores.  Inline asm because the compiler
 // quiets every packed value (v_max_f32 v, v, v) before fmaxf / fmed3 in IEEE mode: the
@@ -158,7 +164,7 @@ __device__ __forceinline__ float dot2_self(uint32_t u, float acc) {
 __device__ __forceinline__ uint32_t lds_addr(const void* p) { return (uint32_t)(uintptr_t)p; }
 
 #ifndef MIVQ_CS_PERMLANE
-#define MIVQ_CS_PERMLANE 1
+#define MIVQ_CS_PERMLANE 0
 #endif
 // Lanes 0..31 receive lane l + 32's value (lanes 32..63: their own value back).  The filter's
 // lane pair (l, l + 32) holds one row; only the h = 0 lanes use the merged result, so a
@@ -263,7 +269,10 @@ __global__ __launch_bounds__(NW * 64) void pq_encode_cs_kernel(
     half8* cimg = reinterpret_cast<half8*>(smem);
     unsigned char* stg_all = smem + FR * 16;
     constexpr int NT = NW * 64;
-    constexpr int kDep = (NW >= kWaves || KH > 1) ? kDepth : 2;  // x blocks in flight per wave
+#ifndef MIVQ_CS_KDEP  // x blocks in flight per wave for the full-occupancy filters (profiling builds: 2)
+#define MIVQ_CS_KDEP 1
+#endif
+    constexpr int kDep = (NW >= kWaves || KH > 1) ? MIVQ_CS_KDEP : 2;  // x blocks in flight per wave
     float* hb = reinterpret_cast<float*>(stg_all + NW * 32 * PITCH);
     float* cnl = hb + 256;
     int* ctr = reinterpret_cast<int*>(cnl + 256);  // [0] pairs, [1] full, [2] resolve batches
@@ -484,6 +493,7 @@ __global__ __launch_bounds__(NW * 64) void pq_encode_cs_kernel(
                 acc[4 * qq + 2] = hv.z; acc[4 * qq + 3] = hv.w;
             }
             constexpr int NP = (KH > 1 && MIVQ_CS_ASPLIT) ? 2 : 1;
+            if (MIVQ_CS_PRIO) __builtin_amdgcn_s_setprio(1);
 #pragma unroll
             for (int part = 0; part < NP; ++part) {
                 half8 a[KS / NP];
@@ -495,30 +505,47 @@ __global__ __launch_bounds__(NW * 64) void pq_encode_cs_kernel(
                     acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(a[ks], bf[part * (KS / NP) + ks], acc, 0, 0, 0);
                 if (NP > 1 && part == 0) __builtin_amdgcn_sched_barrier(0);
             }
+            if (MIVQ_CS_PRIO) __builtin_amdgcn_s_setprio(0);
             return acc;
         };
         if constexpr (NCB > 0) {
+#ifndef MIVQ_CS_NOPIPE  // 1: one accumulator (no MFMAs of block cb + 1 during the ranking of cb)
+#define MIVQ_CS_NOPIPE 0
+#endif
             floatx16 acc_cur = scores(0);
 #pragma unroll
             for (int cb = 0; cb < NCB; ++cb) {
                 floatx16 acc_next;
-                if (cb + 1 < NCB) acc_next = scores(cb + 1);
+                if (!MIVQ_CS_NOPIPE && cb + 1 < NCB) acc_next = scores(cb + 1);
                 if constexpr (kGroups) {
-                    float g1 = -INFINITY, g2 = -INFINITY;
+#ifndef MIVQ_CS_GROUP  // scores per group (8: half the in-group pairs that become full items)
+#define MIVQ_CS_GROUP 16
+#endif
+                    constexpr int GS = MIVQ_CS_GROUP;
 #pragma unroll
-                    for (int i = 0; i < 16; i += 2)
-                        top2_insert2(g1, g2,
-                                     pack_idx(acc_cur[i], vmask, (uint32_t)(cb * 32 + (i & 3) + 8 * (i >> 2))),
-                                     pack_idx(acc_cur[i + 1], vmask,
-                                              (uint32_t)(cb * 32 + ((i + 1) & 3) + 8 * ((i + 1) >> 2))));
-                    merge_group(t1, t2, t3, g1, g2);
+                    for (int g0 = 0; g0 < 16; g0 += GS) {
+                        // a group's first two scores: their max and min (2 ops), then 3 per pair
+                        const float a0 = pack_idx(acc_cur[g0], vmask, (uint32_t)(cb * 32 + (g0 & 3) + 8 * (g0 >> 2)));
+                        const float a1 = pack_idx(acc_cur[g0 + 1], vmask,
+                                                  (uint32_t)(cb * 32 + ((g0 + 1) & 3) + 8 * ((g0 + 1) >> 2)));
+                        float g1, g2;
+                        asm("v_max_f32 %0, %1, %2" : "=v"(g1) : "v"(a0), "v"(a1));
+                        asm("v_min_f32 %0, %1, %2" : "=v"(g2) : "v"(a0), "v"(a1));
+#pragma unroll
+                        for (int i = g0 + 2; i < g0 + GS; i += 2)
+                            top2_insert2(g1, g2,
+                                         pack_idx(acc_cur[i], vmask, (uint32_t)(cb * 32 + (i & 3) + 8 * (i >> 2))),
+                                         pack_idx(acc_cur[i + 1], vmask,
+                                                  (uint32_t)(cb * 32 + ((i + 1) & 3) + 8 * ((i + 1) >> 2))));
+                        merge_group(t1, t2, t3, g1, g2);
+                    }
                 } else {
 #pragma unroll
                     for (int i = 0; i < 16; ++i)
                         top3_insert(t1, t2, t3,
                                     pack_idx(acc_cur[i], vmask, (uint32_t)(cb * 32 + (i & 3) + 8 * (i >> 2))));
                 }
-                if (cb + 1 < NCB) acc_cur = acc_next;
+                if (cb + 1 < NCB) acc_cur = MIVQ_CS_NOPIPE ? scores(cb + 1) : acc_next;
             }
         }
         if constexpr ((V & 16) != 0) {  // keep the loads and conversions alive

@@ -219,6 +219,15 @@ __global__ __launch_bounds__(256) void opq_split_b_kernel(const float* __restric
     bimg[dd + e] = lo;
 }
 
+#ifndef MIVQ_OPQ_XNT
+#define MIVQ_OPQ_XNT 0
+#endif
+typedef float f32x4nt __attribute__((ext_vector_type(4)));
+typedef unsigned int u32x4nt __attribute__((ext_vector_type(4)));
+#ifndef MIVQ_OPQ_BNT
+#define MIVQ_OPQ_BNT 0
+#endif
+
 // Tile t of workgroup b: the workgroups of one XCD (b % 8, dealt round-robin) take a
 // contiguous range of tiles, so consecutive tiles (the column tiles of one row block) share
 // that XCD's L2.
@@ -309,10 +318,24 @@ __global__ __launch_bounds__(WR * WC * 64) void opq_split_gemm_kernel(const floa
         for (int u = 0; u < U; ++u) {
             const int64_t gr = r0 + xrow[u];
             const int k = k0 + xk[u];
-            xv[u] = (gr < n && k < d) ? *reinterpret_cast<const float4*>(x + gr * d + k) : make_float4(0.f, 0.f, 0.f, 0.f);
+            // MIVQ_OPQ_XNT / _BNT (profiling): non-temporal loads of x / of the B image
+            const float* xp = x + gr * d + k;
+            if (MIVQ_OPQ_XNT) {
+                const f32x4nt v = (gr < n && k < d) ? __builtin_nontemporal_load(reinterpret_cast<const f32x4nt*>(xp))
+                                                    : (f32x4nt){0.f, 0.f, 0.f, 0.f};
+                xv[u] = make_float4(v.x, v.y, v.z, v.w);
+            } else {
+                xv[u] = (gr < n && k < d) ? *reinterpret_cast<const float4*>(xp) : make_float4(0.f, 0.f, 0.f, 0.f);
+            }
             const int gc = c0 + bcol[u], kb = k0 + bk[u];
-            bv[u] = (gc < d && kb < d) ? *reinterpret_cast<const uint4*>(bimg + bpl[u] * dd + (int64_t)gc * d + kb)
-                                       : make_uint4(0u, 0u, 0u, 0u);
+            const _Float16* bp = bimg + bpl[u] * dd + (int64_t)gc * d + kb;
+            if (MIVQ_OPQ_BNT) {
+                const u32x4nt v = (gc < d && kb < d) ? __builtin_nontemporal_load(reinterpret_cast<const u32x4nt*>(bp))
+                                                     : (u32x4nt){0u, 0u, 0u, 0u};
+                bv[u] = make_uint4(v.x, v.y, v.z, v.w);
+            } else {
+                bv[u] = (gc < d && kb < d) ? *reinterpret_cast<const uint4*>(bp) : make_uint4(0u, 0u, 0u, 0u);
+            }
         }
     };
     auto sstore = [&](unsigned char* buf) __attribute__((always_inline)) {

@@ -86,6 +86,9 @@ constexpr int kXAux = MIVQ_CS_XAUX;  // x stream cache policy: nt (read once)
 #ifndef MIVQ_CS_PRIO  // profiling: s_setprio 1 around each centroid block's MFMAs
 #define MIVQ_CS_PRIO 0
 #endif
+#ifndef MIVQ_CS_PF  // profiling: dword loads that pull the wave's block after next into L2 (line bytes)
+#define MIVQ_CS_PF 0
+#endif
 
 // Keeps the three largest of a stream of packed scores.  Inline asm because the compiler
 // quiets every packed value (v_max_f32 v, v, v) before fmaxf / fmed3 in IEEE mode: the
@@ -373,9 +376,46 @@ __global__ __launch_bounds__(NW * 64) void pq_encode_cs_kernel(
     int pend_row = -1, pend_k = 0;
     float pend_gap = 0.0f, pend_xs = 0.0f;
     float2 pend_pd = make_float2(0.0f, 0.0f);
-    const float4 b2 = pdw != nullptr ? bnd2[m] : make_float4(0.f, 0.f, 0.f, 0.f);
+    // The pair's load is issued and consumed inside one step (before the refill, settled at the
+    // tail): as a loop-carried load result, the compiler copied it at the loop latch, i.e. waited
+    // vmcnt(0) -- for the next x block's refill too -- at the end of every step.  M > 64 (no
+    // per-pair spreads prepared): every pair goes to the list.
+    constexpr bool kLegacyPairs = (V & (1 << 20)) != 0;  // round-1 pair kernel (profiling)
+    const bool pd_on = pdw != nullptr;
+    const float2* pdsrc = pd_on ? pdw : reinterpret_cast<const float2*>(bnd2);
+    const float4 b2 = pd_on ? bnd2[m] : make_float4(0.f, 0.f, 0.f, 0.f);
+    // The pending pair's spreads: every lane loads (a pair-less lane, or M > 64, reads a valid
+    // 8 B that is never used), so no branch surrounds the load.
+#ifndef MIVQ_CS_PD_EARLY  // 1: the pending pair's load at the next step's start; 0: at the tail
+#define MIVQ_CS_PD_EARLY 1
+#endif
+#ifndef MIVQ_CS_REFILL_COND  // profiling: round-3 conditional refill
+#define MIVQ_CS_REFILL_COND 0
+#endif
+#ifndef MIVQ_CS_PIN
+#define MIVQ_CS_PIN 1
+#endif
+#ifndef MIVQ_CS_D64_R3  // dsub 64 (16 waves at 128 VGPRs): the round-3 loop structure
+#define MIVQ_CS_D64_R3 1
+#endif
+    // dsub 64 keeps the round-3 structure (refill under its branch, the pair load at the tail,
+    // the sigma test per block): with the pinned refill / in-step pair load / per-workgroup
+    // sigma loops its 16-wave register budget spills (20-140 B per lane, measured 3 % slower)
+    // (generic shapes, DS == 0, keep it too: their register budgets differ per KS)
+    constexpr bool kR3Loop = (DS == 64 && NW == 16 && MIVQ_CS_D64_R3) || DS == 0;
+    constexpr bool kPdEarly = MIVQ_CS_PD_EARLY && !kR3Loop;
+    constexpr bool kRefillCond = MIVQ_CS_REFILL_COND || kR3Loop;
+    constexpr bool kPin = MIVQ_CS_PIN && !kR3Loop;
+    auto load_pending_pd = [&]() __attribute__((always_inline)) {
+        if constexpr (!kLegacyPairs) {
+            const bool on = pd_on && pend_row >= 0;
+            pend_pd = pdsrc[((int64_t)(pd_on ? m : 0) * 256 + (on ? (pend_k & 0xFF) : 0)) * 256 +
+                            (on ? (pend_k >> 8) : 0)];
+        }
+    };
     auto settle_pending = [&]() __attribute__((always_inline)) {
         if (pend_row < 0) return false;
+        if (!pd_on) return true;
         const float w12 = 1.0625f * (fmaf(4.8828125e-4f, pend_xs, b2.z) * pend_pd.x + pend_xs * pend_pd.y +
                                      b2.x * pend_xs + b2.y);
         if (pend_gap > w12) {
@@ -404,39 +444,68 @@ __global__ __launch_bounds__(NW * 64) void pq_encode_cs_kernel(
                 const int at = basep + __popcll(bp & below);
                 list[at] = make_uint2((uint32_t)prow, (uint32_t)pk);
                 // the legacy pair kernel's own window needs the score gap and Xs
-                if (pdw == nullptr && pinfo != nullptr) pinfo[(int64_t)m * n + r0 + at] = make_float2(pgap, pxs);
+                if (kLegacyPairs && pinfo != nullptr) pinfo[(int64_t)m * n + r0 + at] = make_float2(pgap, pxs);
             }
             if (isf) list[nrows - 1 - (basef + __popcll(bfull & below))] = make_uint2((uint32_t)frow, 0u);
         }
     };
 
+    // MIVQ_CS_PF = G (profiling): after the refill, one dword per G-byte line of the block after
+    // that goes out (KH == 1), and its value is consumed a step later, so those lines are
+    // in L2 / MALL when the refill of the next step reads them.
+    constexpr int kPfG = MIVQ_CS_PF > 0 ? MIVQ_CS_PF : 64;
+    constexpr int kNpf = (MIVQ_CS_PF > 0 && KH == 1 && DS > 0) ? (32 * DS * 4 / kPfG + 63) / 64 : 0;
+    uint32_t pfv[kNpf > 0 ? kNpf : 1] = {0u};
+    uint32_t pf_sink = 0u;
+    auto prefetch = [&](int pvb) __attribute__((always_inline)) {
+        if constexpr (kNpf > 0) {
+            constexpr int spr = DS * 4 / kPfG;  // lines per row segment
+#pragma unroll
+            for (int j = 0; j < kNpf; ++j) {
+                pf_sink ^= pfv[j];
+                const int s = 64 * j + l, prw = s / spr;
+                const int off = s < 32 * spr ? prw * XS * 4 + (s - prw * spr) * kPfG : (int)0x80000000u;
+                pfv[j] = __builtin_amdgcn_raw_buffer_load_b32(xr_rsrc, off, pvb * 32 * XS * 4, 0);
+            }
+        }
+    };
+
     // One step encodes block vb from registers xr and refills xr with block vb + kDep*NW
     // right after staging it, so kDep blocks per wave are in flight.
-    auto step = [&](const int vb, float4 (&xrh)[KH][NIMAX]) __attribute__((always_inline)) {
+    auto step = [&](auto kScaled, const int vb, float4 (&xrh)[KH][NIMAX]) __attribute__((always_inline)) {
         half8 bf[KS];
         float xx = 0.0f;
 #pragma unroll
         for (int hh = 0; hh < KH; ++hh) {
         float4 (&xr)[NIMAX] = xrh[hh];
-        // sigma * x -> fp16 -> this wave's tile (LAYOUT 0: lanes past the block's rows skip)
-        // sigma == 1 (ordinary codebook magnitudes, pq_prep_mfma_kernel): no scaling multiply
-        if (sigma == 1.0f) {
-#pragma unroll
-            for (int i = 0; i < NIMAX; ++i) {
-                if (i < ni && (LAYOUT != 0 || (lactive && ibase(i) + prow[0] < 32)))
-                    *reinterpret_cast<uint2*>(stg + ibase(i) * PITCH + toff[i % PER]) =
-                        make_uint2(cvt2(xr[i].x, xr[i].y), cvt2(xr[i].z, xr[i].w));
-            }
-        } else {
+        // sigma * x -> fp16 -> this wave's tile (LAYOUT 0: lanes past the block's rows skip).
+        // sigma == 1 (ordinary codebook magnitudes) runs a loop without the multiply; the choice
+        // is made once per workgroup, outside the loop (a uniform branch here made the register
+        // allocator join the x registers of two paths with copies that wait for every load;
+        // kScaled == 2: the round-3 per-block test, kept for dsub 64).
+        auto stage = [&](bool scaled) __attribute__((always_inline)) {
 #pragma unroll
             for (int i = 0; i < NIMAX; ++i) {
                 if (i < ni && (LAYOUT != 0 || (lactive && ibase(i) + prow[0] < 32))) {
-                    const float2v lo = (float2v){xr[i].x, xr[i].y} * sig2;
-                    const float2v hi = (float2v){xr[i].z, xr[i].w} * sig2;
-                    *reinterpret_cast<uint2*>(stg + ibase(i) * PITCH + toff[i % PER]) =
-                        make_uint2(cvt2(lo.x, lo.y), cvt2(hi.x, hi.y));
+                    if (scaled) {
+                        const float2v lo = (float2v){xr[i].x, xr[i].y} * sig2;
+                        const float2v hi = (float2v){xr[i].z, xr[i].w} * sig2;
+                        *reinterpret_cast<uint2*>(stg + ibase(i) * PITCH + toff[i % PER]) =
+                            make_uint2(cvt2(lo.x, lo.y), cvt2(hi.x, hi.y));
+                    } else {
+                        *reinterpret_cast<uint2*>(stg + ibase(i) * PITCH + toff[i % PER]) =
+                            make_uint2(cvt2(xr[i].x, xr[i].y), cvt2(xr[i].z, xr[i].w));
+                    }
                 }
             }
+        };
+        if constexpr (decltype(kScaled)::value == 2) {  // one branch around the whole block
+            if (sigma == 1.0f)
+                stage(false);
+            else
+                stage(true);
+        } else {
+            stage(decltype(kScaled)::value == 1);
         }
         lds_fence();
         if constexpr (KH > 1 && MIVQ_CS_KH_CONTIG) {
@@ -462,8 +531,19 @@ __global__ __launch_bounds__(NW * 64) void pq_encode_cs_kernel(
             xx = dot2_self(u[2], xx); xx = dot2_self(u[3], xx);
         }
         }
-        if (vb + kDep * kProd < nvb && !((V & 64) && vb >= kProd)) load(vb + kDep * kProd, hh, xr);
+        // The refill is unconditional: past the workgroup's last block the range-checked buffer
+        // returns zeros without a memory access.  (Under a branch, the join made the compiler
+        // wait vmcnt(0) at the step's tail for the pair-spread load -- i.e. for this refill too,
+        // so the next block's loads had only one step's compute to land in.)
+        // issued before the refill, so its wait at the tail leaves the refill in flight
+        if (kPdEarly && hh == 0) load_pending_pd();
+        if ((!kRefillCond || vb + kDep * kProd < nvb) && !((V & 64) && vb >= kProd))
+            load(vb + kDep * kProd, hh, xr);
+        // keeps the loads here: the scheduler otherwise sinks them below the MFMAs (shorter
+        // register live ranges), leaving them only the step's tail to land in
+        if (kPin) __builtin_amdgcn_sched_barrier(0);
         }
+        prefetch(vb + (kDep + 1) * kProd);
         xx += upper_half(xx);  // lanes 0..31: the row norm over both halves
 
         // Candidates: the 16 packed scores of centroid block cb in this lane form a group; each
@@ -580,38 +660,32 @@ __global__ __launch_bounds__(NW * 64) void pq_encode_cs_kernel(
         const bool mine = (h == 0) && rowl < nrows;
         if (mine && ncand == 1) codesT[(int64_t)m * n + r0 + rowl] = (uint8_t)k1;
         const float gap = __fmul_rn(__fsub_rn(t1, t2), 0.99999988f);  // rounded down
-        if (pdw != nullptr) {
-            // The previous block's pair (its pd load was issued a whole step ago): k1 is the
-            // code when the gap exceeds the pair's own window, else it goes to the list.
+        if (kR3Loop && !kLegacyPairs && pdw != nullptr) {
+            // round-3 tail (dsub 64, generic shapes): settle the previous block's pair, then
+            // load this block's pair spreads (a runtime branch: M > 64 appends pairs directly)
             const bool listp = settle_pending();
             append(listp, pend_row, pend_k, 0.0f, 0.0f, mine && ncand >= 3, rowl);
-            // Every lane loads (a pair-less lane reads the subspace's first entry) and the state is
-            // selected without branches: a load issued under a branch made the compiler wait
-            // vmcnt(0) at the next block's use -- for the next x block's loads too, issued after it.
-#ifndef MIVQ_CS_PD_UNCOND
-#define MIVQ_CS_PD_UNCOND 1
-#endif
             const bool np = mine && ncand == 2;
-            if (MIVQ_CS_PD_UNCOND) {
-                pend_pd = pdw[((int64_t)m * 256 + (np ? k1 : 0)) * 256 + (np ? k2 : 0)];
-                pend_row = np ? rowl : -1;
-                pend_k = k1 | (k2 << 8);
-                pend_gap = gap;
-                pend_xs = Xs;
-            } else {  // round 3 (profiling builds)
-                pend_row = np ? rowl : -1;
-                if (np) {
-                    pend_k = k1 | (k2 << 8);
-                    pend_gap = gap;
-                    pend_xs = Xs;
-                    pend_pd = pdw[((int64_t)m * 256 + k1) * 256 + k2];
-                }
-            }
+            pend_pd = pdw[((int64_t)m * 256 + (np ? k1 : 0)) * 256 + (np ? k2 : 0)];
+            pend_row = np ? rowl : -1;
+            pend_k = k1 | (k2 << 8);
+            pend_gap = gap;
+            pend_xs = Xs;
+        } else if (!kR3Loop && !kLegacyPairs) {
+            // The previous block's pair (its pd load went out before this block's refill): k1
+            // is the code when the gap exceeds the pair's own window, else it goes to the list.
+            const bool listp = settle_pending();
+            append(listp, pend_row, pend_k, 0.0f, 0.0f, mine && ncand >= 3, rowl);
+            pend_row = mine && ncand == 2 ? rowl : -1;
+            pend_k = k1 | (k2 << 8);
+            pend_gap = gap;
+            pend_xs = Xs;
+            if (!kPdEarly) load_pending_pd();
         } else {
             append(mine && ncand == 2, rowl, k1 | (k2 << 8), gap, Xs, mine && ncand >= 3, rowl);
         }
     };
-    {
+    auto run = [&](auto kScaled) __attribute__((always_inline)) {
         float4 xa[KH][NIMAX], xb[KH][NIMAX];
         int vb = w;
 #pragma unroll
@@ -620,14 +694,30 @@ __global__ __launch_bounds__(NW * 64) void pq_encode_cs_kernel(
             if (kDep == 2 && vb + kProd < nvb) load(vb + kProd, hh, xb[hh]);
         }
         for (; vb < nvb; vb += kDep * kProd) {
-            step(vb, xa);
+            step(kScaled, vb, xa);
             if (kDep == 1) continue;
             if (vb + kProd >= nvb) break;
-            step(vb + kProd, xb);
+            step(kScaled, vb + kProd, xb);
         }
-        if (pdw != nullptr) {
+    };
+    if constexpr (kR3Loop) {
+        run(std::integral_constant<int, 2>{});  // sigma tested per block
+    } else {
+        if (sigma == 1.0f)
+            run(std::integral_constant<int, 0>{});
+        else
+            run(std::integral_constant<int, 1>{});
+    }
+    {
+        if (!kLegacyPairs && (!kR3Loop || pdw != nullptr)) {
+            if (kPdEarly) load_pending_pd();
             const bool listp = settle_pending();
             append(listp, pend_row, pend_k, 0.0f, 0.0f, false, 0);
+        }
+        if constexpr (kNpf > 0) {  // keeps the prefetch loads alive (never true: n >= 0)
+#pragma unroll
+            for (int j = 0; j < kNpf; ++j) pf_sink ^= pfv[j];
+            if (n < 0 && pf_sink == 0x9E3779B9u) codesT[0] = 0;
         }
     }
     }  // producers

@@ -49,6 +49,7 @@ typedef _Float16 half2v __attribute__((ext_vector_type(2)));
 typedef float float2v __attribute__((ext_vector_type(2)));
 typedef float floatx16 __attribute__((ext_vector_type(16)));
 typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 
 #ifndef MIVQ_CS_WAVES
@@ -413,7 +414,29 @@ __global__ __launch_bounds__(NW * 64) void pq_encode_cs_kernel(
                             (on ? (pend_k >> 8) : 0)];
         }
     };
+#ifndef MIVQ_CS_FIXED_STORES  // every step issues the same number of global stores (see below)
+#define MIVQ_CS_FIXED_STORES 0
+#endif
+    // Fixed store count (round-4 loop): the code / list stores of a step go out as buffer stores
+    // from every lane, non-writers with an out-of-range offset (dropped by the range check), and
+    // no branch skips them.  With a data-dependent number of stores the compiler cannot count
+    // them, so the next block's staging waited vmcnt(0) -- for this tail's stores too.
+    constexpr bool kFixedStores = MIVQ_CS_FIXED_STORES && !kR3Loop && !kLegacyPairs;
+    const __amdgpu_buffer_rsrc_t code_rsrc =
+        __builtin_amdgcn_make_buffer_rsrc((void*)(codesT + (int64_t)m * n + r0), 0, nrows, kRsrcWord3);
+    const __amdgpu_buffer_rsrc_t list_rsrc =
+        __builtin_amdgcn_make_buffer_rsrc((void*)(items + (int64_t)m * n + r0), 0, nrows * 8, kRsrcWord3);
+    constexpr int kOob = (int)0x80000000u;
+    // the pending pair, settled or listed without branches (kFixedStores): returns "to the list"
+    auto settle_pending_fixed = [&]() __attribute__((always_inline)) {
+        const float w12 = 1.0625f * (fmaf(4.8828125e-4f, pend_xs, b2.z) * pend_pd.x + pend_xs * pend_pd.y +
+                                     b2.x * pend_xs + b2.y);
+        const bool settled = pend_row >= 0 && pd_on && pend_gap > w12;
+        __builtin_amdgcn_raw_buffer_store_b8((uint8_t)(pend_k & 0xFF), code_rsrc, settled ? pend_row : kOob, 0, 0);
+        return pend_row >= 0 && !settled;
+    };
     auto settle_pending = [&]() __attribute__((always_inline)) {
+        if constexpr (kFixedStores) return settle_pending_fixed();
         if (pend_row < 0) return false;
         if (!pd_on) return true;
         const float w12 = 1.0625f * (fmaf(4.8828125e-4f, pend_xs, b2.z) * pend_pd.x + pend_xs * pend_pd.y +
@@ -430,6 +453,22 @@ __global__ __launch_bounds__(NW * 64) void pq_encode_cs_kernel(
                       __attribute__((always_inline)) {
         const uint64_t bp = __ballot(isp);
         const uint64_t bfull = __ballot(isf);
+        if constexpr (kFixedStores) {
+            int basep = 0, basef = 0;
+            if (l == 0) {  // LDS atomics (lgkmcnt): adding 0 is harmless
+                basep = atomicAdd(&ctr[0], __popcll(bp));
+                basef = atomicAdd(&ctr[1], __popcll(bfull));
+            }
+            basep = __shfl(basep, 0);
+            basef = __shfl(basef, 0);
+            const uint64_t below = (1ull << l) - 1ull;
+            const int atp = basep + __popcll(bp & below);
+            const int atf = nrows - 1 - (basef + __popcll(bfull & below));
+            const u32x2 vp = {(uint32_t)prow, (uint32_t)pk}, vf = {(uint32_t)frow, 0u};
+            __builtin_amdgcn_raw_buffer_store_b64(vp, list_rsrc, isp ? atp * 8 : kOob, 0, 0);
+            __builtin_amdgcn_raw_buffer_store_b64(vf, list_rsrc, isf ? atf * 8 : kOob, 0, 0);
+            return;
+        }
         if (bp | bfull) {
             int basep = 0, basef = 0;
             if (l == 0) {
@@ -658,7 +697,10 @@ __global__ __launch_bounds__(NW * 64) void pq_encode_cs_kernel(
         const int k2 = (int)(__float_as_uint(t2) & 0xFFu);
         const int rowl = vb * 32 + r;
         const bool mine = (h == 0) && rowl < nrows;
-        if (mine && ncand == 1) codesT[(int64_t)m * n + r0 + rowl] = (uint8_t)k1;
+        if constexpr (kFixedStores)
+            __builtin_amdgcn_raw_buffer_store_b8((uint8_t)k1, code_rsrc, mine && ncand == 1 ? rowl : kOob, 0, 0);
+        else if (mine && ncand == 1)
+            codesT[(int64_t)m * n + r0 + rowl] = (uint8_t)k1;
         const float gap = __fmul_rn(__fsub_rn(t1, t2), 0.99999988f);  // rounded down
         if (kR3Loop && !kLegacyPairs && pdw != nullptr) {
             // round-3 tail (dsub 64, generic shapes): settle the previous block's pair, then
@@ -692,6 +734,14 @@ __global__ __launch_bounds__(NW * 64) void pq_encode_cs_kernel(
         for (int hh = 0; hh < KH; ++hh) {
             if (vb < nvb) load(vb, hh, xa[hh]);
             if (kDep == 2 && vb + kProd < nvb) load(vb + kProd, hh, xb[hh]);
+        }
+        if constexpr (kFixedStores) {
+            // the loop's four stores per step, dropped (out of range): the first iteration then
+            // sees the same count of operations after its x loads as every later one
+            __builtin_amdgcn_raw_buffer_store_b8((uint8_t)0, code_rsrc, kOob, 0, 0);
+            __builtin_amdgcn_raw_buffer_store_b8((uint8_t)0, code_rsrc, kOob, 0, 0);
+            __builtin_amdgcn_raw_buffer_store_b64((u32x2){0u, 0u}, list_rsrc, kOob, 0, 0);
+            __builtin_amdgcn_raw_buffer_store_b64((u32x2){0u, 0u}, list_rsrc, kOob, 0, 0);
         }
         for (; vb < nvb; vb += kDep * kProd) {
             step(kScaled, vb, xa);

@@ -228,6 +228,20 @@ typedef unsigned int u32x4nt __attribute__((ext_vector_type(4)));
 #define MIVQ_OPQ_BNT 0
 #endif
 
+// LDS staging line (x row / B column) of staging thread-slot e, 8 slots of 8 B per 64-B line.
+// A 16-lane ds_write_b64 group (or 8-lane ds_write_b128 group) covers two lines; with the 80-B
+// pitch lines j and j + 1 overlap on 4 of the 32 store banks ((a/4) mod 32: 2-way conflicts on
+// every staging store -- the ~577 M conflict cycles per 1M x 1536 rotation in PMC), lines j and
+// j + 4 do not (80 B x 4 = 16 banks apart).  MIVQ_OPQ_WSWZ = 0: the round-3 order (line e / 8).
+#ifndef MIVQ_OPQ_WSWZ
+#define MIVQ_OPQ_WSWZ 0
+#endif
+__device__ __forceinline__ int stage_line(int e) {
+    if (!MIVQ_OPQ_WSWZ) return e >> 3;
+    const int g = e >> 4, sub = (e >> 3) & 1;
+    return (g >> 2) * 8 + (g & 3) + 4 * sub;
+}
+
 // Tile t of workgroup b: the workgroups of one XCD (b % 8, dealt round-robin) take a
 // contiguous range of tiles, so consecutive tiles (the column tiles of one row block) share
 // that XCD's L2.
@@ -298,7 +312,7 @@ __global__ __launch_bounds__(WR * WC * 64) void opq_split_gemm_kernel(const floa
 #pragma unroll
     for (int u = 0; u < U; ++u) {
         const int e = tid + NT * u;
-        xrow[u] = e >> 3;
+        xrow[u] = stage_line(e);
         xk[u] = 4 * (e & 7);
         const int64_t gr = r0 + xrow[u];
         sx[u] = gr < n ? rs[gr] : 0.0f;
@@ -308,7 +322,7 @@ __global__ __launch_bounds__(WR * WC * 64) void opq_split_gemm_kernel(const floa
     for (int u = 0; u < U; ++u) {
         const int e = tid + NT * u;
         bpl[u] = e / (4 * TN);
-        bcol[u] = (e % (4 * TN)) >> 2;
+        bcol[u] = stage_line(2 * (e % (4 * TN)));  // 4 lanes of 16 B per column
         bk[u] = 8 * (e & 3);
     }
     float4 xv[U];

@@ -213,7 +213,16 @@ __device__ __forceinline__ void lds_burst(uint32_t xa, uint32_t ca, f32x4 (&xq)[
 // the grid allows, each XCD gets all M subspaces of a chunk in consecutive slots, so the M
 // workgroups reading one row range run side by side on one XCD and sweep the same DRAM pages
 // together.  Both kernels of the encode use the same mapping (the lists are per workgroup).
+#ifndef MIVQ_CS_XCDM  // profiling: XCD x takes subspaces m = x (mod 8), every chunk (M % 8 == 0)
+#define MIVQ_CS_XCDM 0
+#endif
 __device__ __forceinline__ void wg_coords_of(unsigned b, unsigned g, int M, int& m, int64_t& chunk) {
+    if (MIVQ_CS_XCDM && M % 8 == 0 && g % (8u * (unsigned)M) == 0) {
+        const unsigned j = b >> 3, per = (unsigned)M / 8u;
+        m = (int)((b & 7u) + 8u * (j % per));
+        chunk = (int64_t)(j / per);
+        return;
+    }
     if (g % (8u * (unsigned)M) == 0) {
         const unsigned j = b >> 3;
         m = (int)(j % (unsigned)M);

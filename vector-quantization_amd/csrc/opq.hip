@@ -232,9 +232,9 @@ typedef unsigned int u32x4nt __attribute__((ext_vector_type(4)));
 // A 16-lane ds_write_b64 group (or 8-lane ds_write_b128 group) covers two lines; with the 80-B
 // pitch lines j and j + 1 overlap on 4 of the 32 store banks ((a/4) mod 32: 2-way conflicts on
 // every staging store -- the ~577 M conflict cycles per 1M x 1536 rotation in PMC), lines j and
-// j + 4 do not (80 B x 4 = 16 banks apart).  MIVQ_OPQ_WSWZ = 0: the round-3 order (line e / 8).
+// j + 4 do not (80 B x 4 = 16 banks apart).  MIVQ_OPQ_WSWZ = 0: the round-3 order (line e / 8); measured 16.16 -> 16.01 ms per rotation.
 #ifndef MIVQ_OPQ_WSWZ
-#define MIVQ_OPQ_WSWZ 0
+#define MIVQ_OPQ_WSWZ 1
 #endif
 __device__ __forceinline__ int stage_line(int e) {
     if (!MIVQ_OPQ_WSWZ) return e >> 3;

@@ -51,3 +51,27 @@ def test_select_per_pass_and_missing(tmp_path):
     vals, _, grid = select(str(tmp_path), "opq_split_gemm", 3)
     assert grid == 8 and vals["FETCH_SIZE"] == [1.0] and vals["WRITE_SIZE"] == [2.0]
     assert select(str(tmp_path), "no_such_kernel", 3) == ({}, [], None)
+
+
+def test_gpurunignore_keeps_what_the_gpu_runs_read():
+    """bench.py reads profiles/traffic.json on the GPU box (roofline.traffic); the library and the
+    golden fixtures must travel too.  tar --exclude semantics: a pattern matches a member path
+    (wildcards match '/'), and excluding a directory excludes everything under it."""
+    import fnmatch
+
+    root = Path(__file__).resolve().parents[1]
+    pats = [p.strip() for p in (root / ".gpurunignore").read_text().splitlines() if p.strip()]
+
+    def excluded(rel):
+        parts = rel.split("/")
+        prefixes = ["./" + "/".join(parts[:i]) for i in range(1, len(parts) + 1)]
+        for p in pats:
+            for cand in prefixes:
+                if fnmatch.fnmatch(cand, p) or (not p.startswith("./") and fnmatch.fnmatch(cand.split("/")[-1], p)):
+                    return True
+        return False
+
+    for rel in ("profiles/traffic.json", "vector-quantization_amd/lib/libmivq.so", "bench.py",
+                "tests/golden/sq_golden_wide.npz", "oracle/mivq_oracle.c", "include/mivq.h"):
+        assert not excluded(rel), rel
+    assert excluded("profiles/r04_s11/bench_default.log")

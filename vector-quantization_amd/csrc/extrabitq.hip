@@ -147,14 +147,28 @@ constexpr int kRotAP = kRotK + 1;   // A stage row pitch (doubles): [row][k]
 constexpr int kRotBP = kRotT + 1;   // B stage row pitch (doubles): [k][col]
 typedef double f64x4 __attribute__((ext_vector_type(4)));
 
+// Tile of workgroup b.  MIVQ_ERQ_XCD (default): the workgroups of one XCD (b % 8, dealt
+// round-robin) take a contiguous range of tiles, so the column tiles of one 128-row block run
+// side by side on one XCD and share its L2 copy of the o strip (3 MB at D = 3072); the round-3
+// order (b itself) spread them over all eight XCDs, each fetching the strip again.
+#ifndef MIVQ_ERQ_XCD
+#define MIVQ_ERQ_XCD 1
+#endif
+__device__ __forceinline__ int64_t erq_tile(int64_t b, int64_t G) {
+    if (!MIVQ_ERQ_XCD) return b;
+    const int64_t x = b & 7, j = b >> 3, q = G >> 3, r = G & 7;
+    return x * q + (x < r ? x : r) + j;
+}
+
 __global__ __launch_bounds__(256) void erq_rotate_kernel(const double* __restrict__ o, int64_t n, int d,
                                                          const double* __restrict__ P, int transpose,
                                                          double* __restrict__ s, int64_t ctiles) {
     __shared__ double As[2][kRotT * kRotAP];
     __shared__ double Bs[2][kRotK * kRotBP];
     const int tid = threadIdx.x, l = tid & 63, w = tid >> 6;
-    const int64_t r0 = (int64_t)(blockIdx.x / ctiles) * kRotT;
-    const int c0 = (int)(blockIdx.x % ctiles) * kRotT;
+    const int64_t t = erq_tile(blockIdx.x, gridDim.x);
+    const int64_t r0 = (t / ctiles) * kRotT;
+    const int c0 = (int)(t % ctiles) * kRotT;
     const int wr = w >> 1, wc = w & 1;  // wave tile: rows wr*64.., cols wc*64..
     f64x4 acc[4][4];
 #pragma unroll

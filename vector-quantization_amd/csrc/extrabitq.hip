@@ -249,6 +249,111 @@ __global__ __launch_bounds__(256) void erq_rotate_kernel(const double* __restric
                 if (row < n && col < d) s[row * d + col] = acc[a][b][g];
             }
 }
+
+// d % 32 == 0 (every BASELINE width): the same tile, slices and MFMA order as erq_rotate_kernel
+// (identical results), with the global side rebuilt: each thread's 8-double chunks are in or out
+// of range as a whole, so they load as 16-B buffer loads (range-checked: rows past n read zeros,
+// no branches), and the loads run TWO slices ahead through two register stages (slice ks + 2
+// loads while slice ks computes; slice ks + 1, loaded a slice earlier, goes to LDS after it).
+// The generic kernel's per-element guarded 8-B loads compiled to a branch per load and a
+// vmcnt(0) in the middle of its loads.
+typedef unsigned int erq_u32x4 __attribute__((ext_vector_type(4)));
+template <int TR>
+__global__ __launch_bounds__(256, 2) void erq_rotate_fast_kernel(const double* __restrict__ o, int64_t n, int d,
+                                                              const double* __restrict__ P,
+                                                              double* __restrict__ s, int64_t ctiles) {
+    __shared__ double As[2][kRotT * kRotAP];
+    __shared__ double Bs[2][kRotK * kRotBP];
+    const int tid = threadIdx.x, l = tid & 63, w = tid >> 6;
+    const int64_t t = erq_tile(blockIdx.x, gridDim.x);
+    const int64_t r0 = (t / ctiles) * kRotT;
+    const int c0 = (int)(t % ctiles) * kRotT;
+    const int wr = w >> 1, wc = w & 1;
+    f64x4 acc[4][4];
+#pragma unroll
+    for (int a = 0; a < 4; ++a)
+#pragma unroll
+        for (int b = 0; b < 4; ++b) acc[a][b] = (f64x4){0.0, 0.0, 0.0, 0.0};
+    constexpr int kOob = (int)0x80000000u;
+    const int rows = (int)(n - r0 < kRotT ? n - r0 : kRotT);
+    // o rows r0 .. r0 + rows of this tile (< 4 GiB: 128 rows); P whole (d^2 * 8 < 2^31 checked)
+    const __amdgpu_buffer_rsrc_t ors =
+        __builtin_amdgcn_make_buffer_rsrc((void*)(o + r0 * d), 0, rows * d * 8, 0x00020000);
+    const __amdgpu_buffer_rsrc_t prs = __builtin_amdgcn_make_buffer_rsrc((void*)P, 0, d * d * 8, 0x00020000);
+    const int ar = tid >> 1, ak = 8 * (tid & 1);                        // A: row, k offset
+    const int bk = TR ? 8 * (tid & 1) : tid >> 4, bj = TR ? tid >> 1 : 8 * (tid & 15);  // B
+    auto gload = [&](int k0, double (&ra)[8], double (&rb)[8]) __attribute__((always_inline)) {
+        const int va = k0 + ak < d ? (ar * d + k0 + ak) * 8 : kOob;
+        const int vb = TR ? ((c0 + bj < d && k0 + bk < d) ? ((c0 + bj) * d + k0 + bk) * 8 : kOob)
+                          : ((k0 + bk < d && c0 + bj < d) ? ((k0 + bk) * d + c0 + bj) * 8 : kOob);
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const erq_u32x4 ua = __builtin_amdgcn_raw_buffer_load_b128(ors, va == kOob ? kOob : va + 16 * q, 0, 0);
+            const erq_u32x4 ub = __builtin_amdgcn_raw_buffer_load_b128(prs, vb == kOob ? kOob : vb + 16 * q, 0, 0);
+            ra[2 * q] = __hiloint2double((int)ua[1], (int)ua[0]);
+            ra[2 * q + 1] = __hiloint2double((int)ua[3], (int)ua[2]);
+            rb[2 * q] = __hiloint2double((int)ub[1], (int)ub[0]);
+            rb[2 * q + 1] = __hiloint2double((int)ub[3], (int)ub[2]);
+        }
+    };
+    auto sstore = [&](int st, const double (&ra)[8], const double (&rb)[8]) __attribute__((always_inline)) {
+#pragma unroll
+        for (int u = 0; u < 8; ++u) As[st][ar * kRotAP + ak + u] = ra[u];
+        if (TR) {
+#pragma unroll
+            for (int u = 0; u < 8; ++u) Bs[st][(bk + u) * kRotBP + bj] = rb[u];
+        } else {
+#pragma unroll
+            for (int u = 0; u < 8; ++u) Bs[st][bk * kRotBP + bj + u] = rb[u];
+        }
+    };
+    const int fi = l & 15, fk = l >> 4;
+    auto slice = [&](int st) __attribute__((always_inline)) {
+#pragma unroll
+        for (int k4 = 0; k4 < kRotK; k4 += 4) {
+            double af[4], bf[4];
+#pragma unroll
+            for (int a = 0; a < 4; ++a) af[a] = As[st][(wr * 64 + a * 16 + fi) * kRotAP + k4 + fk];
+#pragma unroll
+            for (int b = 0; b < 4; ++b) bf[b] = Bs[st][(k4 + fk) * kRotBP + wc * 64 + b * 16 + fi];
+#pragma unroll
+            for (int a = 0; a < 4; ++a)
+#pragma unroll
+                for (int b = 0; b < 4; ++b)
+                    acc[a][b] = __builtin_amdgcn_mfma_f64_16x16x4f64(af[a], bf[b], acc[a][b], 0, 0, 0);
+        }
+    };
+    const int nk = (d + kRotK - 1) / kRotK;
+    double ra0[8], rb0[8], ra1[8], rb1[8];
+    gload(0, ra0, rb0);
+    gload(kRotK, ra1, rb1);
+    sstore(0, ra0, rb0);
+    __syncthreads();
+    // two slices per trip (nk is even: d % 32 == 0) so the register stages stay static and no
+    // branch splits the loop: slice ks computes from LDS stage 0 while slice ks + 2 loads into
+    // the stage slice ks came from; loads past d read zeros, and the last trip's stores of them
+    // into stage 0 are never read
+    for (int ks = 0; ks < nk; ks += 2) {
+        gload((ks + 2) * kRotK, ra0, rb0);
+        slice(0);
+        sstore(1, ra1, rb1);
+        __syncthreads();
+        gload((ks + 3) * kRotK, ra1, rb1);
+        slice(1);
+        sstore(0, ra0, rb0);
+        __syncthreads();
+    }
+#pragma unroll
+    for (int a = 0; a < 4; ++a)
+#pragma unroll
+        for (int b = 0; b < 4; ++b)
+#pragma unroll
+            for (int g = 0; g < 4; ++g) {
+                const int64_t row = r0 + wr * 64 + a * 16 + fk + 4 * g;
+                const int col = c0 + wc * 64 + b * 16 + fi;
+                if (row < n && col < d) s[row * d + col] = acc[a][b][g];
+            }
+}
 }  // namespace
 }  // namespace mivq
 
@@ -306,7 +411,20 @@ extern "C" int mivq_extrabitq_rotate(const double* o, int64_t n, int32_t d, cons
     MIVQ_REQUIRE(o && P && s && o != s, MIVQ_ERR_INVALID, "extrabitq_rotate: null or aliased pointer");
     const int64_t ct = ceil_div(d, kRotT), tiles = ceil_div(n, kRotT) * ct;
     MIVQ_REQUIRE(tiles < ((int64_t)1 << 31), MIVQ_ERR_UNSUPPORTED, "extrabitq_rotate: n=%lld too large", (long long)n);
-    hipLaunchKernelGGL(erq_rotate_kernel, dim3((unsigned)tiles), dim3(256), 0, as_stream(stream), o, n, d, P, transpose, s,
-                       ct);
+#ifndef MIVQ_ERQ_FAST
+#define MIVQ_ERQ_FAST 1
+#endif
+    // the fast kernel's buffer offsets are 32-bit: d^2 * 8 bytes of P and 128 rows of o
+    if (MIVQ_ERQ_FAST && d % 32 == 0 && (int64_t)d * d * 8 < ((int64_t)1 << 31)) {
+        if (transpose)
+            hipLaunchKernelGGL(erq_rotate_fast_kernel<1>, dim3((unsigned)tiles), dim3(256), 0, as_stream(stream), o, n, d,
+                               P, s, ct);
+        else
+            hipLaunchKernelGGL(erq_rotate_fast_kernel<0>, dim3((unsigned)tiles), dim3(256), 0, as_stream(stream), o, n, d,
+                               P, s, ct);
+    } else {
+        hipLaunchKernelGGL(erq_rotate_kernel, dim3((unsigned)tiles), dim3(256), 0, as_stream(stream), o, n, d, P,
+                           transpose, s, ct);
+    }
     return check_launch("extrabitq_rotate");
 }

@@ -222,6 +222,9 @@ __global__ __launch_bounds__(256) void opq_split_b_kernel(const float* __restric
 #ifndef MIVQ_OPQ_XNT
 #define MIVQ_OPQ_XNT 0
 #endif
+#ifndef MIVQ_OPQ_BUF
+#define MIVQ_OPQ_BUF 1
+#endif
 typedef float f32x4nt __attribute__((ext_vector_type(4)));
 typedef unsigned int u32x4nt __attribute__((ext_vector_type(4)));
 #ifndef MIVQ_OPQ_BNT
@@ -327,9 +330,26 @@ __global__ __launch_bounds__(WR * WC * 64) void opq_split_gemm_kernel(const floa
     }
     float4 xv[U];
     uint4 bv[U];
+    // MIVQ_OPQ_BUF: range-checked 16-B buffer loads (rows past n read zeros; a chunk past d gets
+    // an out-of-range offset) instead of one guarded load per chunk, which compiled to a branch
+    // per load (15.93 -> 14.80 ms per 1M x 1536 rotation, profiles/r04_s14); 32-bit offsets
+    // from the tile's first row (4 d^2 < 2^31 checked at launch)
+    constexpr int kOob = (int)0x80000000u;
+    const int trows = (int)(n - r0 < TM ? n - r0 : TM);
+    const __amdgpu_buffer_rsrc_t xrs =
+        __builtin_amdgcn_make_buffer_rsrc((void*)(x + r0 * d), 0, trows * d * 4, 0x00020000);
+    const __amdgpu_buffer_rsrc_t brs = __builtin_amdgcn_make_buffer_rsrc((void*)bimg, 0, (int)(dd * 4), 0x00020000);
     auto gload = [&](int k0) __attribute__((always_inline)) {
 #pragma unroll
         for (int u = 0; u < U; ++u) {
+            if (MIVQ_OPQ_BUF) {
+                const int k = k0 + xk[u], gc = c0 + bcol[u], kb = k0 + bk[u];
+                const int vx = k < d ? (xrow[u] * d + k) * 4 : kOob;
+                const int vb = (gc < d && kb < d) ? (int)((bpl[u] * dd + (int64_t)gc * d + kb) * 2) : kOob;
+                xv[u] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(xrs, vx, 0, 0));
+                bv[u] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(brs, vb, 0, 0));
+                continue;
+            }
             const int64_t gr = r0 + xrow[u];
             const int k = k0 + xk[u];
             // MIVQ_OPQ_XNT / _BNT (profiling): non-temporal loads of x / of the B image
@@ -788,6 +808,9 @@ extern "C" int mivq_opq_rotate_prepared(const float* x, int64_t n, int32_t d, co
                  workspace_bytes, need);
     MIVQ_REQUIRE(reinterpret_cast<uintptr_t>(workspace) % 16 == 0, MIVQ_ERR_INVALID,
                  "opq_rotate_prepared: workspace must be 16-byte aligned");
+    // the split GEMM's buffer offsets are 32-bit (MIVQ_OPQ_BUF): the B image is 4 d^2 bytes
+    MIVQ_REQUIRE(!MIVQ_OPQ_BUF || (int64_t)4 * d * d < ((int64_t)1 << 31), MIVQ_ERR_UNSUPPORTED,
+                 "opq_rotate_prepared: d=%d too large", d);
     hipStream_t st = as_stream(stream);
     float* rs = static_cast<float*>(workspace);
     const float* hdr = static_cast<const float*>(prep);

@@ -382,6 +382,26 @@ def test_rabitq_parity(dev, oracle, n, d, metric):
     np.testing.assert_array_equal(rec, oracle.rabitq_decode(got, d))  # same code row -> same floats
 
 
+@pytest.mark.parametrize("n,d", [(300, 1024), (129, 1536), (257, 3072), (65, 2048), (40, 520)])
+def test_rabitq_parity_with_centroid(dev, oracle, n, d):
+    """The centroid path of every rabitq_encode kernel (the batched-load kernel at d % 512 == 0
+    with 2 / 3 / 6 / 4 bytes per lane, the generic kernel at d = 520): sign bits exact, factors
+    within the 1e-5 contract of the sequential restatement."""
+    from haag_vq import _native
+
+    rng = np.random.default_rng(d + 1)
+    X = rng.standard_normal((n, d)).astype(np.float32)
+    c = (0.1 * rng.standard_normal(d)).astype(np.float32)
+    X[1] = c  # residual exactly zero
+    ref = oracle.rabitq_encode(X, c, metric=1)
+    got = _h(_native.rabitq_encode(_t(X, dev), _t(c, dev), 1))
+    nb = (d + 7) // 8
+    np.testing.assert_array_equal(got[:, :nb], ref[:, :nb])
+    f_ref = ref[:, nb:].copy().view(np.float32)
+    f_got = got[:, nb:].copy().view(np.float32)
+    np.testing.assert_allclose(f_got, f_ref, rtol=1e-5, atol=1e-5 * np.abs(f_ref).max())
+
+
 @pytest.mark.parametrize("nq,n,d,M,nbits,k", [
     (37, 5000, 1536, 16, 8, 10),
     (9, 3000, 1536, 32, 8, 100),

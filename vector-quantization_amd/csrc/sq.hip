@@ -132,10 +132,14 @@ __global__ __launch_bounds__(256) void sq_encode_f32_vec_kernel(const float* __r
     for (int64_t rbk = blockIdx.y; rbk * kSqRows < n; rbk += gridDim.y) {
     const int64_t r0 = rbk * kSqRows + (threadIdx.x >> 6);
     const int64_t r1 = min(n, (rbk + 1) * kSqRows);
-    for (int64_t i0 = r0; i0 < r1; i0 += 16) {
-        float4 xa[4], xb[4];
+#ifndef MIVQ_SQ_DEPTH  // rows per wave whose loads are in flight together
+#define MIVQ_SQ_DEPTH 4  // 8: 3.75 vs 2.98 ms per 1M x 3072 (profiles/r04_s15)
+#endif
+    constexpr int SQD = MIVQ_SQ_DEPTH;
+    for (int64_t i0 = r0; i0 < r1; i0 += 4 * SQD) {
+        float4 xa[SQD], xb[SQD];
 #pragma unroll
-        for (int k = 0; k < 4; ++k) {
+        for (int k = 0; k < SQD; ++k) {
             const int64_t i = i0 + 4 * k;
             if (i < r1) {
                 const float4* xr = reinterpret_cast<const float4*>(x + i * (uint64_t)d + j0);
@@ -144,7 +148,7 @@ __global__ __launch_bounds__(256) void sq_encode_f32_vec_kernel(const float* __r
             }
         }
 #pragma unroll
-        for (int k = 0; k < 4; ++k) {
+        for (int k = 0; k < SQD; ++k) {
             const int64_t i = i0 + 4 * k;
             if (i >= r1) break;
             const float xv[8] = {xa[k].x, xa[k].y, xa[k].z, xa[k].w, xb[k].x, xb[k].y, xb[k].z, xb[k].w};

@@ -464,7 +464,7 @@ def flatcodes_leg(a, dev, kind, steps, warmup, cpu=True):
     else:
         enc = lambda: _native.rabitq_encode(X, None, _native.METRIC_L2)  # noqa: E731
         dec = lambda c: _native.rabitq_decode(c, d, None)  # noqa: E731
-        bpv, kname = 4 * d + d // 8 + 8, "rabitq_encode_kernel"
+        bpv, kname = 4 * d + d // 8 + 8, "rabitq_encode_wide_kernel<6>"
     wall, dev_ms = timed(enc, steps, warmup)
     codes = enc()
     # this box's streaming rates on the same bytes (torch device copy: read + write; sum: read):
@@ -576,7 +576,7 @@ def extrabitq_leg(a, dev, steps, warmup, cpu=True):
            "value": n / wall, "unit": "vectors/s", "ms_per_step": wall * 1e3, "dtype": "f64",
            "config": {"workload": f"extrabitq{nbits}_roundtrip_{n}x{d}", "num_bits": nbits, "fit_s": t_fit,
                       "encode_ms": enc_ms, "step": "compress + decompress"},
-           "roofline": {"bound": "mfma", "kernel": "erq_rotate_kernel (v_mfma_f64_16x16x4_f64, o . P)",
+           "roofline": {"bound": "mfma", "kernel": "erq_rotate_fast_kernel (v_mfma_f64_16x16x4_f64, o . P)",
                         "achieved": tfs, "peak": MFMA_F64_PEAK_TFS, "unit": "TFLOP/s", "frac": tfs / MFMA_F64_PEAK_TFS,
                         "rotate_ms": rot_ms, "rotate_transposed_ms": rotT_ms, "flops_per_launch": flops,
                         "flops_per_vector": 2 * d * d,

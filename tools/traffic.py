@@ -25,7 +25,7 @@ WORKLOADS = {
     "pq8_encode_1000000x1536": ["pq_encode_cs_kernelILi12ELi3ELi0ELi192", "pq_resolve_merged_kernelILi12ELi192"],
     "opq32_rotate_1000000x1536": ["opq_row_scale_kernel", "opq_split_gemm_kernel"],
     "sq8_encode_1000000x3072": ["sq_encode_f32_vec_kernel"],
-    "rabitq1_encode_1000000x3072": ["rabitq_encode_kernel<true>"],
+    "rabitq1_encode_1000000x3072": ["rabitq_encode_wide_kernel"],  # d % 512 == 0 (rabitq.hip)
 }
 
 

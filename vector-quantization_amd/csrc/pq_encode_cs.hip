@@ -87,6 +87,9 @@ constexpr int kXAux = MIVQ_CS_XAUX;  // x stream cache policy: nt (read once)
 #ifndef MIVQ_CS_PRIO  // profiling: s_setprio 1 around each centroid block's MFMAs
 #define MIVQ_CS_PRIO 0
 #endif
+#ifndef MIVQ_CS_NOPIPE  // 1: one accumulator everywhere (no MFMAs of block cb + 1 during the ranking of cb)
+#define MIVQ_CS_NOPIPE 0
+#endif
 #ifndef MIVQ_CS_PF  // profiling: dword loads that pull the wave's block after next into L2 (line bytes)
 #define MIVQ_CS_PF 0
 #endif
@@ -405,14 +408,18 @@ __global__ __launch_bounds__(NW * 64) void pq_encode_cs_kernel(
 #ifndef MIVQ_CS_PIN
 #define MIVQ_CS_PIN 1
 #endif
-#ifndef MIVQ_CS_D64_R3  // dsub 64 (16 waves at 128 VGPRs): the round-3 loop structure
-#define MIVQ_CS_D64_R3 1
+#ifndef MIVQ_CS_D64_R3  // profiling: dsub 64 (16 waves at 128 VGPRs) on the round-3 loop structure
+#define MIVQ_CS_D64_R3 0
 #endif
-    // dsub 64 keeps the round-3 structure (refill under its branch, the pair load at the tail,
-    // the sigma test per block): with the pinned refill / in-step pair load / per-workgroup
-    // sigma loops its 16-wave register budget spills (20-140 B per lane, measured 3 % slower)
-    // (generic shapes, DS == 0, keep it too: their register budgets differ per KS)
+    // dsub 64 at 16 waves: the round-4 loop with both accumulators spills (20-140 B per lane,
+    // 3 % slower), so that kernel runs it with ONE accumulator (kNoPipe: the next centroid
+    // block's MFMAs wait for this block's ranking; the other three waves of the SIMD overlap
+    // them): 122 VGPRs, 6.52 -> 6.47 ms per 6.65M x 1024 call (profiles/r04_s19).  With
+    // MIVQ_CS_D64_R3 it keeps round 3's structure (refill under its branch, the pair load at
+    // the tail, the sigma test per block), as the generic shapes (DS == 0) do: their register
+    // budgets differ per KS.
     constexpr bool kR3Loop = (DS == 64 && NW == 16 && MIVQ_CS_D64_R3) || DS == 0;
+    constexpr bool kNoPipe = MIVQ_CS_NOPIPE || (DS == 64 && NW == 16 && !MIVQ_CS_D64_R3);
     constexpr bool kPdEarly = MIVQ_CS_PD_EARLY && !kR3Loop;
     constexpr bool kRefillCond = MIVQ_CS_REFILL_COND || kR3Loop;
     constexpr bool kPin = MIVQ_CS_PIN && !kR3Loop;
@@ -637,14 +644,12 @@ __global__ __launch_bounds__(NW * 64) void pq_encode_cs_kernel(
             return acc;
         };
         if constexpr (NCB > 0) {
-#ifndef MIVQ_CS_NOPIPE  // 1: one accumulator (no MFMAs of block cb + 1 during the ranking of cb)
-#define MIVQ_CS_NOPIPE 0
-#endif
+
             floatx16 acc_cur = scores(0);
 #pragma unroll
             for (int cb = 0; cb < NCB; ++cb) {
                 floatx16 acc_next;
-                if (!MIVQ_CS_NOPIPE && cb + 1 < NCB) acc_next = scores(cb + 1);
+                if (!kNoPipe && cb + 1 < NCB) acc_next = scores(cb + 1);
                 if constexpr (kGroups) {
 #ifndef MIVQ_CS_GROUP  // scores per group (8: half the in-group pairs that become full items)
 #define MIVQ_CS_GROUP 16
@@ -673,7 +678,7 @@ __global__ __launch_bounds__(NW * 64) void pq_encode_cs_kernel(
                         top3_insert(t1, t2, t3,
                                     pack_idx(acc_cur[i], vmask, (uint32_t)(cb * 32 + (i & 3) + 8 * (i >> 2))));
                 }
-                if (cb + 1 < NCB) acc_cur = MIVQ_CS_NOPIPE ? scores(cb + 1) : acc_next;
+                if (cb + 1 < NCB) acc_cur = kNoPipe ? scores(cb + 1) : acc_next;
             }
         }
         if constexpr ((V & 16) != 0) {  // keep the loads and conversions alive

@@ -225,6 +225,12 @@ __global__ __launch_bounds__(256) void opq_split_b_kernel(const float* __restric
 #ifndef MIVQ_OPQ_BUF
 #define MIVQ_OPQ_BUF 1
 #endif
+#ifndef MIVQ_OPQ_SFIRST  // split-and-store of step s + 1 before step s's MFMAs (14.80 -> 14.27 ms, r04_s22)
+#define MIVQ_OPQ_SFIRST 1
+#endif
+#ifndef MIVQ_OPQ_UNCOND  // profiling: the loop's load / store without the last-step branches
+#define MIVQ_OPQ_UNCOND 0
+#endif
 typedef float f32x4nt __attribute__((ext_vector_type(4)));
 typedef unsigned int u32x4nt __attribute__((ext_vector_type(4)));
 #ifndef MIVQ_OPQ_BNT
@@ -402,11 +408,23 @@ __global__ __launch_bounds__(WR * WC * 64) void opq_split_gemm_kernel(const floa
     const int nsteps = (d + SBK - 1) / SBK;
     gload(0);
     sstore(smem);
+    // MIVQ_OPQ_SFIRST: step s + 1's chunks (loaded during step s - 1) go to LDS at the START of
+    // step s, then step s + 2's loads are issued, then step s's MFMAs -- the loads have a whole
+    // step to land and the store no longer sits between the MFMAs and the barrier; loads past d
+    // read zeros (buffer loads), so no branch surrounds them (the last steps' stores are never read)
+    if (MIVQ_OPQ_SFIRST && MIVQ_OPQ_BUF) gload(SBK);
     __syncthreads();
     const int fr = l & 31, fk = 16 * (l >> 5);  // fragment row / col and byte offset of its k-group
     for (int s = 0; s < nsteps; ++s) {
         unsigned char* cur = smem + (s & 1) * T::BUF;
-        if (s + 1 < nsteps) gload((s + 1) * SBK);
+        if (MIVQ_OPQ_SFIRST && MIVQ_OPQ_BUF) {
+            sstore(smem + ((s + 1) & 1) * T::BUF);
+            gload((s + 2) * SBK);
+        } else if (MIVQ_OPQ_UNCOND && MIVQ_OPQ_BUF) {
+            gload((s + 1) * SBK);
+        } else if (s + 1 < nsteps) {
+            gload((s + 1) * SBK);
+        }
 #pragma unroll
         for (int kk = 0; kk < 2; ++kk) {
             half8 ah[RB], al[RB], bh[CB], bl[CB];
@@ -436,7 +454,8 @@ __global__ __launch_bounds__(WR * WC * 64) void opq_split_gemm_kernel(const floa
 #pragma unroll
                 for (int b = 0; b < CB; ++b) acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[a], bh[b], acc[a][b], 0, 0, 0);
         }
-        if (s + 1 < nsteps) sstore(smem + ((s + 1) & 1) * T::BUF);
+        if (!(MIVQ_OPQ_SFIRST && MIVQ_OPQ_BUF) && (MIVQ_OPQ_UNCOND && MIVQ_OPQ_BUF || s + 1 < nsteps))
+            sstore(smem + ((s + 1) & 1) * T::BUF);
         __syncthreads();
     }
     // epilogue (the staging buffers are reused: every wave must be done with them)

@@ -154,6 +154,9 @@ typedef double f64x4 __attribute__((ext_vector_type(4)));
 #ifndef MIVQ_ERQ_XCD
 #define MIVQ_ERQ_XCD 1
 #endif
+#ifndef MIVQ_ERQ_SFIRST  // stage-first loop order in erq_rotate_fast_kernel (61.8 -> 58.6 ms, r04_s25)
+#define MIVQ_ERQ_SFIRST 1
+#endif
 __device__ __forceinline__ int64_t erq_tile(int64_t b, int64_t G) {
     if (!MIVQ_ERQ_XCD) return b;
     const int64_t x = b & 7, j = b >> 3, q = G >> 3, r = G & 7;
@@ -328,6 +331,22 @@ __global__ __launch_bounds__(256, 2) void erq_rotate_fast_kernel(const double* _
     gload(0, ra0, rb0);
     gload(kRotK, ra1, rb1);
     sstore(0, ra0, rb0);
+    if (MIVQ_ERQ_SFIRST) {
+        // stage first: each half-trip stores the next slice (loaded a half-trip and more ago)
+        // BEFORE its MFMAs, then issues the loads of the slice three ahead into the freed stage
+        gload(2 * kRotK, ra0, rb0);
+        __syncthreads();
+        for (int ks = 0; ks < nk; ks += 2) {
+            sstore(1, ra1, rb1);                 // slice ks + 1
+            gload((ks + 3) * kRotK, ra1, rb1);
+            slice(0);                            // slice ks
+            __syncthreads();
+            sstore(0, ra0, rb0);                 // slice ks + 2 (past nk: zeros, never read)
+            gload((ks + 4) * kRotK, ra0, rb0);
+            slice(1);                            // slice ks + 1
+            __syncthreads();
+        }
+    } else {
     __syncthreads();
     // two slices per trip (nk is even: d % 32 == 0) so the register stages stay static and no
     // branch splits the loop: slice ks computes from LDS stage 0 while slice ks + 2 loads into
@@ -342,6 +361,7 @@ __global__ __launch_bounds__(256, 2) void erq_rotate_fast_kernel(const double* _
         slice(1);
         sstore(0, ra0, rb0);
         __syncthreads();
+    }
     }
 #pragma unroll
     for (int a = 0; a < 4; ++a)

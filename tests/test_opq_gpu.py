@@ -163,3 +163,30 @@ def test_polar_factor_newton_schulz(dev):
     Qd = polar_factor(_t(Gd, dev)).cpu().numpy()
     np.testing.assert_allclose(Qd.T @ Qd, np.eye(d), atol=1e-10)
     np.testing.assert_allclose(Qd @ (Qd.T @ Gd), Gd, atol=1e-10)
+
+
+@pytest.mark.gpu
+def test_polar_factor_top_vector_orthogonal_to_ones(dev):
+    """G whose dominant right singular vector is orthogonal to the all-ones vector
+    and whose top two singular values are 2 : 1.  A start scale estimated from below (a power
+    iteration from ones / sqrt(d)) would put the top value near 1.8 > sqrt(3), where
+    Newton-Schulz converges to -1: an orthogonal matrix that is NOT the polar factor.  The
+    upper-bound scale must give U V^T."""
+    from haag_vq.methods.optimized_product_quantization import polar_factor
+
+    rng = np.random.default_rng(11)
+    d = 64
+    U, _ = np.linalg.qr(rng.standard_normal((d, d)))
+    v1 = np.zeros(d)
+    v1[0], v1[1] = 2 ** -0.5, -(2 ** -0.5)  # orthogonal to ones
+    V = np.linalg.qr(np.column_stack([v1, rng.standard_normal((d, d - 1))]))[0]  # V[:, 0] = +-v1
+    assert abs(V[:, 0] @ np.ones(d)) < 1e-12
+    S = np.ones(d)
+    S[0] = 2.0
+    G = (U * S) @ V.T
+    Q = polar_factor(_t(G, dev)).cpu().numpy()
+    np.testing.assert_allclose(Q, U @ V.T, atol=1e-9)
+    # Q^T G is the symmetric positive definite factor V S V^T
+    P = Q.T @ G
+    np.testing.assert_allclose(P, P.T, atol=1e-9)
+    assert np.linalg.eigvalsh((P + P.T) / 2).min() > 0.5

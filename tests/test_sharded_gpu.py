@@ -1,0 +1,94 @@
+"""Multi-rank paths on one GPU (VERDICT r4 "put config #5 behind the product's own
+caller"): two ranks share the card and exchange over gloo on host copies.  The RCCL path is the
+same code with backend "nccl" (bench.py --gpus N).
+
+* `vq-benchmark streaming-sweep --gpus 2`: the logged MSE / counts equal the single-process run
+  bit for bit, and the row carries n_gpus / device / roofline_frac.
+* ShardedFlatIndex: the global top-k of two row shards equals the single-device ranking of the
+  whole database (ids and distances), L2 and IP, k = 10 and k = 300, with exact duplicates
+  across the shard boundary.
+"""
+import json
+import os
+import sqlite3
+import subprocess
+import sys
+from pathlib import Path
+
+import numpy as np
+import pytest
+
+ROOT = Path(__file__).resolve().parents[1]
+PKG = ROOT / "vector-quantization_amd"
+
+
+def _env():
+    return dict(os.environ, PYTHONPATH=str(PKG), VQ_DIST_BACKEND="gloo", OMP_NUM_THREADS="1",
+                HSA_ENABLE_IPC_MODE_LEGACY="0")
+
+
+def _rows(db):
+    con = sqlite3.connect(db)
+    rows = con.execute("SELECT metrics_json, config_json, sweep_id FROM runs").fetchall()
+    con.close()
+    return [(json.loads(m), json.loads(c), s) for m, c, s in rows]
+
+
+@pytest.mark.gpu
+def test_streaming_sweep_two_ranks_one_gpu(dev, tmp_path):
+    X = np.random.default_rng(9).standard_normal((20003, 128)).astype(np.float32)
+    f = tmp_path / "stream.npy"
+    np.save(f, X)
+    out = {}
+    for g in (1, 2):
+        db = tmp_path / f"runs{g}.db"
+        cmd = [sys.executable, "-u", "-m", "haag_vq", "streaming-sweep", "--method", "pq", "--pq-subquantizers", "8",
+               "--training-size", "8192", "--batch-size", "3000", "--data-path", str(f), "--db-path", str(db),
+               "--gpus", str(g)]
+        p = subprocess.run(cmd, capture_output=True, text=True, env=_env(), timeout=300, cwd=str(tmp_path))
+        assert p.returncode == 0, p.stdout[-3000:] + p.stderr[-3000:]
+        rows = _rows(db)
+        assert len(rows) == 1  # rank 0 logs the run once
+        out[g] = rows[0]
+    (m1, c1, _), (m2, c2, _) = out[1], out[2]
+    assert m1["total_vectors_compressed"] == m2["total_vectors_compressed"] == 20003
+    assert m1["num_batches"] == m2["num_batches"] == 7
+    assert m1["mse"] == m2["mse"]  # bit for bit
+    assert m1["n_gpus"] == 1 and m2["n_gpus"] == 2 and c2["n_gpus"] == 2 and c2["M"] == 8
+    for m in (m1, m2):
+        assert m["device"] and 0.0 < m["roofline_frac"] < 1.0 and m["encode_vectors_per_s"] > 0
+
+
+@pytest.mark.gpu
+def test_sharded_flat_index_two_ranks_one_gpu(dev, tmp_path):
+    res_file = tmp_path / "res.json"
+    from haag_vq.parallel.launch import free_port
+
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
+           "--master-addr=127.0.0.1", f"--master-port={free_port()}", str(ROOT / "tests" / "_sharded_worker.py"),
+           str(res_file)]
+    p = subprocess.run(cmd, capture_output=True, text=True, env=_env(), timeout=300, cwd=str(tmp_path))
+    assert p.returncode == 0, p.stdout[-3000:] + p.stderr[-3000:]
+    res = json.loads(res_file.read_text())
+    assert res["world"] == 2
+    for metric in ("l2", "ip"):
+        r = res[metric]
+        assert r["sharded_ids"] == r["single_ids"], metric
+        assert np.array_equal(np.array(r["sharded_d"], np.float32), np.array(r["single_d"], np.float32)), metric
+        assert r["k300_ids"] == r["k300_single_ids"], metric
+    assert res["l2"]["sharded_ids"][0][:3] == [5, 17, 30008]  # exact duplicates: by id across the shards
+
+
+@pytest.mark.gpu
+def test_sweep_logs_device_fields(dev, tmp_path):
+    from haag_vq.benchmarks.sweep import sweep
+
+    db = tmp_path / "s.db"
+    sweep(method="sq", dataset="dummy", num_samples=2000, dim=64, dataset_limit=None, cache_dir=str(tmp_path),
+          pq_subquantizers="8", pq_bits="8", sq_bits="8", rabitq_metric_type="L2", saq_num_bits="4",
+          saq_total_bits="", saq_allowed_bits="", saq_segments="", opq_quantizers="8", opq_bits="8",
+          with_recall=False, with_pairwise=False, with_rank=False, num_pairs=10, rank_k=10, ground_truth_path=None,
+          codebooks_dir=str(tmp_path / "cb"), db_path=str(db), gpus=1, device=None)
+    (m, c, _), = _rows(db)
+    assert m["n_gpus"] == 1 and c["n_gpus"] == 1 and m["device"] == c["device"]
+    assert m["encode_device_ms"] > 0 and 0.0 < m["roofline_frac"] < 1.0

@@ -41,10 +41,11 @@ from haag_vq.methods.rabit_quantization import RaBitQuantizer
 from haag_vq.methods.scalar_quantization import ScalarQuantizer
 from haag_vq.metrics.distortion import compute_distortion
 from haag_vq.metrics.pairwise_distortion import compute_pairwise_distortion
-from haag_vq.metrics.performance import measure_qps, time_compress, time_decompress
+from haag_vq.metrics.performance import device_encode_roofline, measure_qps, time_compress, time_decompress
 from haag_vq.metrics.rank_distortion import compute_rank_distortion
 from haag_vq.metrics.recall import evaluate_recall
 from haag_vq.utils.faiss_utils import MetricType
+from haag_vq.parallel.launch import finish_rank, init_rank, launch_ranks, launched_world
 from haag_vq.utils.run_logger import log_run
 
 DATASETS = ("dummy", "huggingface", "cohere-msmarco", "dbpedia-100k", "dbpedia-1536", "dbpedia-3072")
@@ -75,6 +76,8 @@ def sweep(
     ground_truth_path: str = typer.Option(None, help="Path to precomputed ground truth (.npy file)"),
     codebooks_dir: str = typer.Option(None, help="Directory to save codebooks (default: ./codebooks or $CODEBOOKS_DIR)"),
     db_path: str = typer.Option(None, help="Path to SQLite database (default: logs/benchmark_runs.db or $DB_PATH)"),
+    gpus: int = typer.Option(1, help="GPUs of this node: one process per GPU, the configurations dealt round-robin"),
+    device: int = typer.Option(None, help="GPU index for a single-process sweep (default: the current device)"),
 ) -> str:
     """Run a parameter sweep and log every configuration to the run database.
 
@@ -82,6 +85,30 @@ def sweep(
         vq-benchmark sweep --method pq --dataset dummy --pq-subquantizers 8 --pq-bits 8
         vq-benchmark sweep --method sq --dataset dummy
     """
+    if gpus > 1 and launched_world() == 1:
+        # one process per GPU as a child command, before anything here touches the GPU
+        sweep_id = f"sweep_{datetime.now().strftime('%Y%m%d_%H%M%S')}_{uuid.uuid4().hex[:8]}"
+        args = ["sweep", "--method", method, "--dataset", dataset, "--num-samples", str(num_samples), "--dim", str(dim),
+                "--cache-dir", cache_dir, "--pq-subquantizers", pq_subquantizers, "--pq-bits", pq_bits,
+                "--sq-bits", sq_bits, "--rabitq-metric-type", rabitq_metric_type,
+                "--opq-quantizers", opq_quantizers, "--opq-bits", opq_bits,
+                "--num-pairs", str(num_pairs), "--rank-k", str(rank_k), "--gpus", str(gpus)]
+        args += ["--with-recall" if with_recall else "--no-with-recall",
+                 "--with-pairwise" if with_pairwise else "--no-with-pairwise",
+                 "--with-rank" if with_rank else "--no-with-rank"]
+        for flag, v in (("--dataset-limit", dataset_limit), ("--ground-truth-path", ground_truth_path),
+                        ("--codebooks-dir", codebooks_dir), ("--db-path", db_path)):
+            if v is not None:
+                args += [flag, str(v)]
+        rc = launch_ranks(gpus, args, extra_env={"VQ_SWEEP_ID": sweep_id})
+        if rc != 0:
+            raise RuntimeError(f"sweep: the {gpus}-rank run exited with {rc}")
+        return sweep_id
+    world = launched_world()
+    if world > 1 and gpus != world:
+        raise ValueError(f"sweep: --gpus {gpus} but WORLD_SIZE={world}")
+    info = init_rank(device)
+
     if codebooks_dir is None:
         codebooks_dir = os.getenv("CODEBOOKS_DIR")
     codebooks_dir = Path(codebooks_dir) if codebooks_dir is not None else Path.cwd() / "codebooks"
@@ -93,7 +120,7 @@ def sweep(
         precomputed_gt = np.load(ground_truth_path, allow_pickle=False)
         print(f"   Loaded ground truth shape: {precomputed_gt.shape}")
 
-    sweep_id = f"sweep_{datetime.now().strftime('%Y%m%d_%H%M%S')}_{uuid.uuid4().hex[:8]}"
+    sweep_id = os.environ.get("VQ_SWEEP_ID") or f"sweep_{datetime.now().strftime('%Y%m%d_%H%M%S')}_{uuid.uuid4().hex[:8]}"
     print("=" * 70)
     print("  HAAG Vector Quantization - Parameter Sweep (MI355X)")
     print("=" * 70)
@@ -123,13 +150,16 @@ def sweep(
     else:
         raise ValueError(f"Unknown method: {method}. Supported: pq, sq, rabitq, opq, saq")
 
-    print(f"\nRunning {len(configs)} configurations...")
+    print(f"\nRunning {len(configs)} configurations..." + (f" (rank {info.rank} of {info.world})" if info.world > 1 else ""))
     print("-" * 70)
     for i, config in enumerate(configs, 1):
+        if (i - 1) % info.world != info.rank:  # --gpus N: configuration i runs on rank (i - 1) mod N
+            continue
         print(f"\n[{i}/{len(configs)}] {config['name']}")
         _run_single_config(method=method, dataset=dataset, data=data, config=config, with_recall=with_recall,
                            with_pairwise=with_pairwise, with_rank=with_rank, num_pairs=num_pairs, rank_k=rank_k,
-                           sweep_id=sweep_id, codebooks_dir=codebooks_dir, db_path=db_path)
+                           sweep_id=sweep_id, codebooks_dir=codebooks_dir, db_path=db_path, n_gpus=info.world)
+    finish_rank(info)
     print("\n" + "=" * 70)
     print(f"  Sweep complete: {len(configs)} configurations, sweep id {sweep_id}")
     print(f"  Results logged to: {db_path or os.getenv('DB_PATH', 'logs/benchmark_runs.db')}")
@@ -211,8 +241,11 @@ def _build_model(method: str, config: Dict[str, Any]):
 
 def _run_single_config(method: str, dataset: str, data: Dataset, config: Dict[str, Any], with_recall: bool,
                        with_pairwise: bool, with_rank: bool, num_pairs: int, rank_k: int, sweep_id: str = None,
-                       codebooks_dir: Path = None, db_path: str = None) -> Dict[str, Any]:
-    """Fit, encode, decode and score one configuration; log it; return its metrics."""
+                       codebooks_dir: Path = None, db_path: str = None, n_gpus: int = 1) -> Dict[str, Any]:
+    """Fit, encode, decode and score one configuration; log it; return its metrics.  Besides
+    the reference's fields, metrics_json carries ``device``, ``encode_device_ms`` and
+    ``roofline_frac`` (the device encode of X against the 8 TB/s HBM roofline) and config_json
+    ``n_gpus`` and ``device``."""
     model = _build_model(method, config)
     X = data.vectors
     t0 = perf_counter()
@@ -244,6 +277,9 @@ def _run_single_config(method: str, dataset: str, data: Dataset, config: Dict[st
     metrics.update(measure_qps(data.queries, model=model, codebook_vectors=_get_codebook_vectors(model)))
     if with_recall:
         metrics.update(evaluate_recall(data, model, num_queries=100))
+    metrics.update(device_encode_roofline(model, X))
+    metrics["n_gpus"] = int(n_gpus)
+    config = dict(config, n_gpus=int(n_gpus), device=metrics.get("device"))
 
     log_run(method=method, dataset=dataset, metrics=metrics, config=config, sweep_id=sweep_id, db_path=db_path)
 

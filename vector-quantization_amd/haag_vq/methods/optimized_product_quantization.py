@@ -91,32 +91,27 @@ def polar_factor(G: torch.Tensor, tol: float = 1e-13, max_iter: int = 60) -> tor
     """The orthogonal polar factor Q = U V^T of a square fp64 matrix G = U S V^T (what
     faiss OPQMatrix::train takes from its SVD), by the Newton-Schulz iteration
     Q <- Q (3 I - Q^T Q) / 2 on the fp64 MFMA GEMM (erq_rotate_kernel) instead of rocsolver's
-    SVD.  Start: G scaled by 1.1 x a power-iteration estimate of its largest singular value
-    (the iteration converges for singular values in (0, sqrt(3))); it doubles the digits once
-    every singular value is near 1, and stops at ||Q^T Q - I||_F < tol sqrt(d) or once that
-    error stalls at the fp64 rounding floor of the GEMMs.  A G the iteration cannot orthogonalise
-    (rank deficient, or not converged within max_iter: condition numbers far beyond 1e8) falls
-    back to the SVD."""
+    SVD.  Start: G divided by an UPPER bound of its largest singular value,
+    min(||G||_F, sqrt(||G^T G||_inf)), so every scaled singular value lies in (0, 1] and the
+    iteration takes each of them to +1 (a start value above sqrt(3) goes to -1 or diverges, and
+    an estimate from below -- e.g. a power iteration whose start vector misses the top singular
+    vector -- cannot rule that out).  It doubles the digits once every singular value is near 1,
+    and stops at ||Q^T Q - I||_F < tol sqrt(d) or once that error stalls at the fp64 rounding
+    floor of the GEMMs.  A G the iteration cannot orthogonalise (rank deficient, or not
+    converged within max_iter: condition numbers far beyond 1e8) falls back to the SVD."""
     d = G.shape[0]
     I = torch.eye(d, dtype=torch.float64, device=G.device)
-    v = torch.ones((d,), dtype=torch.float64, device=G.device) / d ** 0.5
     GtG = _mm(G.T, G)
-    smax2 = 0.0
-    for _ in range(12):  # power iteration on G^T G (element-wise + row sums: no BLAS call)
-        w = (GtG * v.view(1, d)).sum(dim=1)
-        smax2 = float(w.norm())
-        if not smax2 > 0.0:
-            break
-        v = w / smax2
-    if smax2 > 0.0 and smax2 < float("inf"):
-        Q = G / (1.1 * smax2 ** 0.5)
+    bound = min(float(G.norm()), float(GtG.abs().sum(dim=1).max()) ** 0.5)
+    if bound > 0.0 and bound < float("inf"):
+        Q = G / bound
         prev = float("inf")
         for _ in range(max_iter):
             T = _mm(Q.T, Q)
             err = float((T - I).norm())
             if err < tol * d ** 0.5 or (err < 1e-8 and err > 0.25 * prev):
                 return Q  # converged (quadratic phase stalled: the rounding floor)
-            if not err < 1e3:  # diverging or non-finite
+            if not err < 1e3:  # non-finite
                 break
             prev = err
             Q = 1.5 * Q - 0.5 * _mm(Q, T)

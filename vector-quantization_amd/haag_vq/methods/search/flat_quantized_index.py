@@ -37,18 +37,21 @@ from ..scalar_quantization import ScalarQuantizer
 _METRIC = {"l2": _native.METRIC_L2, "ip": _native.METRIC_INNER_PRODUCT}
 
 
-def search_codes(model: BaseQuantizer, codes, Q, k: int, metric: str = "l2") -> Tuple[torch.Tensor, torch.Tensor]:
+def search_codes(model: BaseQuantizer, codes, Q, k: int, metric: str = "l2",
+                 id_offset: int = 0) -> Tuple[torch.Tensor, torch.Tensor]:
     """Top-k of queries Q against encoded database ``codes`` of ``model`` (device tensors).
 
     Returns (dists f32 (nq, k), ids int32 (nq, k) holding uint32 ids); IP distances are
-    returned as inner products (descending).
+    returned as inner products (descending).  ``id_offset`` is added to every id (the first
+    global row of a database shard, parallel/sharded.py).
     """
     mt = _METRIC[metric]
     Qd = _arrays.to_device(Q)
     cd = codes if _arrays.is_tensor(codes) else torch.from_numpy(np.ascontiguousarray(codes))
     cd = cd.to(_arrays.device())
     if k > MAX_KERNEL_K:
-        return _search_large_k(model, cd, Qd, k, mt)
+        d, i = _search_large_k(model, cd, Qd, k, mt)
+        return d, (i.to(torch.int64) + id_offset).to(torch.int32) if id_offset else i
     if isinstance(model, (ProductQuantizer, OptimizedProductQuantizer)):
         pq = model if isinstance(model, ProductQuantizer) else model.inner
         if isinstance(model, OptimizedProductQuantizer):
@@ -56,11 +59,11 @@ def search_codes(model: BaseQuantizer, codes, Q, k: int, metric: str = "l2") -> 
         cd = cd.to(torch.uint8).contiguous()
         u8 = cd if pq.B == 8 else _native.pq_unpack(cd, pq.M, pq.B)
         lut = _native.adc_lut(Qd, pq.centroids_device, pq.B, mt)
-        d, i = _native.adc_search(lut, u8, k, pq.B)
+        d, i = _native.adc_search(lut, u8, k, pq.B, id_offset=id_offset)
     else:
         xh = model.decompress(cd)
         xh = _arrays.to_device(xh, torch.float32)
-        d, i = _native.flat_search(Qd, xh, k, mt)
+        d, i = _native.flat_search(Qd, xh, k, mt, id_offset=id_offset)
     if mt == _native.METRIC_INNER_PRODUCT:
         d = -d
     return d, i
@@ -91,6 +94,47 @@ def _search_large_k(model, cd, Qd, k: int, mt: int) -> Tuple[torch.Tensor, torch
 
 def ids_to_numpy(i: torch.Tensor) -> np.ndarray:
     return _arrays.to_host(i).view(np.uint32)
+
+
+def quantizer_state(q: BaseQuantizer) -> dict:
+    """A fitted quantizer as plain numpy arrays (index files; the rank-0 -> all-ranks
+    broadcast of parallel/sharded.py)."""
+    if isinstance(q, ProductQuantizer):
+        return dict(qtype=np.array("pq"), M=np.array(q.M), B=np.array(q.B), centroids=_arrays.to_host(q._C))
+    if isinstance(q, OptimizedProductQuantizer):
+        return dict(qtype=np.array("opq"), M=np.array(q.M), B=np.array(q.B), A=_arrays.to_host(q.opq.A_device),
+                    centroids=_arrays.to_host(q.inner._C))
+    if isinstance(q, ScalarQuantizer):
+        return dict(qtype=np.array("sq"), num_bits=np.array(q.num_bits), min=np.asarray(q.min), max=np.asarray(q.max))
+    if isinstance(q, RaBitQuantizer):
+        return dict(qtype=np.array("rabitq"), metric_type=np.array(int(q.metric_type)), d=np.array(q.rabitq.d))
+    raise ValueError(f"save(): unsupported quantizer {type(q).__name__}")
+
+
+def quantizer_from_state(z) -> BaseQuantizer:
+    """Inverse of quantizer_state (z: a mapping of numpy arrays, e.g. an open .npz)."""
+    qt = str(z["qtype"])
+    if qt == "pq":
+        q = ProductQuantizer(M=int(z["M"]), B=int(z["B"]))
+        q.set_codebooks(z["centroids"])
+    elif qt == "opq":
+        q = OptimizedProductQuantizer(M=int(z["M"]), B=int(z["B"]))
+        q.opq = OPQHandle(_arrays.to_device(z["A"]))
+        inner = ProductQuantizer(M=int(z["M"]), B=int(z["B"]))
+        inner.set_codebooks(z["centroids"])
+        q._inner = inner
+        q.pq = inner.pq
+    elif qt == "sq":
+        q = ScalarQuantizer(num_bits=int(z["num_bits"]))
+        q.min = np.array(z["min"])
+        q.max = np.array(z["max"])
+    elif qt == "rabitq":
+        from ...utils.faiss_utils import MetricType
+        q = RaBitQuantizer(metric_type=MetricType(int(z["metric_type"])))
+        q.fit(np.empty((0, int(z["d"])), dtype=np.float32))
+    else:
+        raise ValueError(f"load(): unknown quantizer type {qt!r}")
+    return q
 
 
 class FlatQuantizedIndex(BaseSearchIndex):
@@ -145,20 +189,9 @@ class FlatQuantizedIndex(BaseSearchIndex):
 
     # --------------------------------------------------------------- persistence
     def _state(self) -> dict:
-        q = self._quantizer
         st = {"codes": _arrays.to_host(self._codes), "metric": np.array(self._metric),
               "N": np.array(self._N), "D": np.array(self._D)}
-        if isinstance(q, ProductQuantizer):
-            st.update(qtype=np.array("pq"), M=np.array(q.M), B=np.array(q.B), centroids=_arrays.to_host(q._C))
-        elif isinstance(q, OptimizedProductQuantizer):
-            st.update(qtype=np.array("opq"), M=np.array(q.M), B=np.array(q.B), A=_arrays.to_host(q.opq.A_device),
-                      centroids=_arrays.to_host(q.inner._C))
-        elif isinstance(q, ScalarQuantizer):
-            st.update(qtype=np.array("sq"), num_bits=np.array(q.num_bits), min=np.asarray(q.min), max=np.asarray(q.max))
-        elif isinstance(q, RaBitQuantizer):
-            st.update(qtype=np.array("rabitq"), metric_type=np.array(int(q.metric_type)), d=np.array(q.rabitq.d))
-        else:
-            raise ValueError(f"save(): unsupported quantizer {type(q).__name__}")
+        st.update(quantizer_state(self._quantizer))
         return st
 
     def save(self, path: str | Path) -> None:
@@ -169,27 +202,7 @@ class FlatQuantizedIndex(BaseSearchIndex):
 
     def load(self, path: str | Path) -> None:
         with np.load(Path(path), allow_pickle=False) as z:
-            qt = str(z["qtype"])
-            if qt == "pq":
-                q = ProductQuantizer(M=int(z["M"]), B=int(z["B"]))
-                q.set_codebooks(z["centroids"])
-            elif qt == "opq":
-                q = OptimizedProductQuantizer(M=int(z["M"]), B=int(z["B"]))
-                q.opq = OPQHandle(_arrays.to_device(z["A"]))
-                inner = ProductQuantizer(M=int(z["M"]), B=int(z["B"]))
-                inner.set_codebooks(z["centroids"])
-                q._inner = inner
-                q.pq = inner.pq
-            elif qt == "sq":
-                q = ScalarQuantizer(num_bits=int(z["num_bits"]))
-                q.min = np.array(z["min"])
-                q.max = np.array(z["max"])
-            elif qt == "rabitq":
-                from ...utils.faiss_utils import MetricType
-                q = RaBitQuantizer(metric_type=MetricType(int(z["metric_type"])))
-                q.fit(np.empty((0, int(z["d"])), dtype=np.float32))
-            else:
-                raise ValueError(f"load(): unknown quantizer type {qt!r}")
+            q = quantizer_from_state(z)
             self._quantizer = q
             self._codes = torch.from_numpy(np.array(z["codes"])).to(_arrays.device())
             self._metric = str(z["metric"])

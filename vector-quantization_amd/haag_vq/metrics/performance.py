@@ -36,6 +36,34 @@ def time_decompress(model: BaseQuantizer, codes) -> Tuple[np.ndarray, float]:
     return rec, float(perf_counter() - t0)
 
 
+HBM_PEAK_BYTES_PER_S = 8.0e12  # MI355X HBM3E
+
+
+def device_encode_roofline(model: BaseQuantizer, X, reps: int = 3) -> Dict[str, object]:
+    """Device time of ``model.compress`` on device-resident rows (HIP events, best of ``reps``
+    after one warm-up) and its fraction of the HBM roofline: (bytes of X read + code bytes
+    written) / time / 8 TB/s.  Logged next to the reference's host-timed latencies
+    (the ``device`` / ``n_gpus`` / ``roofline_frac`` fields)."""
+    if not torch.cuda.is_available():
+        return {}
+    Xd = X if isinstance(X, torch.Tensor) else torch.from_numpy(np.ascontiguousarray(X))
+    Xd = Xd.to(torch.cuda.current_device())
+    codes = model.compress(Xd)
+    best = float("inf")
+    for _ in range(max(1, reps)):
+        s_, e_ = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        s_.record()
+        codes = model.compress(Xd)
+        e_.record()
+        e_.synchronize()
+        best = min(best, s_.elapsed_time(e_) * 1e-3)
+    cb = codes.numel() * codes.element_size() if isinstance(codes, torch.Tensor) else int(np.asarray(codes).nbytes)
+    nbytes = Xd.numel() * Xd.element_size() + cb
+    return {"device": torch.cuda.get_device_name(torch.cuda.current_device()),
+            "encode_device_ms": best * 1e3,
+            "roofline_frac": nbytes / best / HBM_PEAK_BYTES_PER_S if best > 0 else None}
+
+
 def measure_qps(queries, *, model: Optional[BaseQuantizer] = None, codebook_vectors: Optional[np.ndarray] = None,
                 codebook_path: Optional[str] = None, repeats: int = 3, topk: int = 1) -> Dict[str, float]:
     """Reference "QPS" proxy: codebook query (PQ-like / SQ) or compress(queries) (RaBitQ)."""

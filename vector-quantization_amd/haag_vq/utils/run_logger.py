@@ -51,7 +51,7 @@ def log_run(method, dataset, metrics: dict, config: dict = None, sweep_id: str =
     except Exception:
         pkg_version = "mivq-dev"
     cli = " ".join(shlex.quote(a) for a in sys.argv)
-    con = sqlite3.connect(db_path)
+    con = sqlite3.connect(db_path, timeout=120)  # ranks of `--gpus N` share the file
     cur = con.cursor()
     cur.execute(
         "CREATE TABLE IF NOT EXISTS runs (id INTEGER PRIMARY KEY AUTOINCREMENT, timestamp TEXT, "

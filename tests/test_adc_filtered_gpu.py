@@ -1,0 +1,128 @@
+"""The filtered ADC search (adc.hip: integer-LUT scan + exact fp32 re-rank + certificate, the
+fp32 scan re-run on uncertified queries) returns exactly the canonical top-k of
+FlatQuantizedIndex.search_with_scores' ADC counterpart
+(/root/reference/src/haag_vq/methods/search/flat_quantized_index.py:45-76): the oracle's
+answer and the library's fp32-only scan (MIVQ_ADC_EXACT=1), bit for bit, on inputs built to
+defeat the filter (every row the same code, a handful of distinct rows, near-equal LUT
+entries, non-finite LUTs) and on the shape edges (k = 64 / 65 / 256, M = 32 up to k = 192,
+ragged query blocks, id offsets).  MIVQ_ADC_NO_FALLBACK=1 (a test hook) skips the re-run, which
+shows the certificate really carries the ordinary cases and really refuses the adversarial
+ones."""
+import os
+
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+
+def _t(a, dev):
+    return torch.from_numpy(np.ascontiguousarray(a)).to(dev)
+
+
+def _h(t):
+    return t.detach().cpu().numpy()
+
+
+def _search(lut_d, codes_d, k, id_offset=0, env=None):
+    from haag_vq import _native
+
+    keys = ("MIVQ_ADC_EXACT", "MIVQ_ADC_NO_FALLBACK")
+    old = {k_: os.environ.pop(k_, None) for k_ in keys}
+    try:
+        os.environ.update(env or {})
+        d, i = _native.adc_search(lut_d, codes_d, k, 8, id_offset=id_offset)
+        torch.cuda.synchronize()
+        return _h(d), _h(i).view(np.uint32)
+    finally:
+        for k_ in keys:
+            os.environ.pop(k_, None)
+            if old[k_] is not None:
+                os.environ[k_] = old[k_]
+
+
+def _check(dev, oracle, lut, u8, k, id_offset=0):
+    d_ref, i_ref = oracle.adc_search(lut, u8, k, id_offset)
+    lut_d, codes_d = _t(lut, dev), _t(u8, dev)
+    d_f, i_f = _search(lut_d, codes_d, k, id_offset)
+    d_e, i_e = _search(lut_d, codes_d, k, id_offset, {"MIVQ_ADC_EXACT": "1"})
+    np.testing.assert_array_equal(d_f, d_ref)
+    np.testing.assert_array_equal(i_f, i_ref)
+    np.testing.assert_array_equal(d_e, d_ref)
+    np.testing.assert_array_equal(i_e, i_ref)
+    return lut_d, codes_d, d_ref, i_ref
+
+
+def _lut(oracle, rng, nq, M, dsub, metric=1):
+    C = rng.standard_normal((M, 256, dsub)).astype(np.float32)
+    Q = rng.standard_normal((nq, M * dsub)).astype(np.float32)
+    return oracle.adc_lut(Q, C, metric)
+
+
+@pytest.mark.parametrize("M,k", [(16, 1), (16, 10), (16, 64), (16, 65), (16, 256), (32, 10), (32, 192), (32, 193)])
+@pytest.mark.parametrize("metric", [1, 0])
+def test_filtered_adc_shapes(dev, oracle, M, k, metric):
+    rng = np.random.default_rng(M * 1000 + k)
+    nq, n = 37, 20011
+    lut = _lut(oracle, rng, nq, M, 8, metric)
+    u8 = rng.integers(0, 256, size=(n, M)).astype(np.uint8)
+    u8[n - 1] = u8[0]  # duplicate rows far apart: id tie-break
+    u8[n // 2] = u8[0]
+    lut_d, codes_d, d_ref, i_ref = _check(dev, oracle, lut, u8, k, id_offset=123457)
+    if M == 16 and k <= 64:
+        # ordinary data: every query certified by the filter alone
+        d_n, i_n = _search(lut_d, codes_d, k, 123457, {"MIVQ_ADC_NO_FALLBACK": "1"})
+        np.testing.assert_array_equal(i_n, i_ref)
+        np.testing.assert_array_equal(d_n, d_ref)
+
+
+def test_filtered_adc_all_rows_identical(dev, oracle):
+    """Every row the same code: every part's list is full of equal keys, no certificate can
+    hold -- all queries go to the fp32 re-run, and the answer is rows 0..k-1."""
+    rng = np.random.default_rng(1)
+    nq, n, M, k = 21, 30000, 16, 10
+    lut = _lut(oracle, rng, nq, M, 4)
+    u8 = np.tile(rng.integers(0, 256, size=(1, M)).astype(np.uint8), (n, 1))
+    lut_d, codes_d, d_ref, i_ref = _check(dev, oracle, lut, u8, k)
+    assert (i_ref == np.arange(k, dtype=np.uint32)).all()
+    d_n, i_n = _search(lut_d, codes_d, k, 0, {"MIVQ_ADC_NO_FALLBACK": "1"})
+    assert not np.array_equal(i_n, i_ref)  # the filter alone does not vouch for them
+
+
+def test_filtered_adc_few_distinct_rows_and_near_ties(dev, oracle):
+    """A handful of distinct code rows (massive ties) and LUT entries that differ by a few ulps
+    (every row inside the quantisation window)."""
+    rng = np.random.default_rng(2)
+    nq, n, M, k = 19, 25000, 16, 17
+    lut = _lut(oracle, rng, nq, M, 4)
+    base = rng.integers(0, 256, size=(5, M)).astype(np.uint8)
+    u8 = base[rng.integers(0, 5, size=n)]
+    _check(dev, oracle, lut, u8, k)
+    near = np.full((nq, M, 256), 0.5, np.float32)
+    near += rng.integers(0, 4, size=near.shape).astype(np.float32) * np.float32(2 ** -24)
+    near[3] *= np.float32(1e30)  # one query with huge entries
+    near[4] *= np.float32(1e-30)  # and one with tiny ones
+    u8 = rng.integers(0, 256, size=(n, M)).astype(np.uint8)
+    _check(dev, oracle, near, u8, k)
+
+
+def test_filtered_adc_nonfinite_luts(dev, oracle):
+    """+inf / NaN entries: those queries take the fp32 scan (NaN distances rank as +inf)."""
+    rng = np.random.default_rng(3)
+    nq, n, M, k = 18, 6000, 16, 10
+    lut = _lut(oracle, rng, nq, M, 4)
+    lut[2, 5, :] = np.inf
+    lut[7, 0, 17] = np.nan
+    lut[9, 3, 200] = -np.inf
+    u8 = rng.integers(0, 256, size=(n, M)).astype(np.uint8)
+    _check(dev, oracle, lut, u8, k)
+
+
+@pytest.mark.parametrize("n", [1, 9, 1023, 4097])
+def test_filtered_adc_small_databases(dev, oracle, n):
+    rng = np.random.default_rng(n)
+    nq, M, k = 33, 16, 10
+    lut = _lut(oracle, rng, nq, M, 4)
+    u8 = rng.integers(0, 256, size=(n, M)).astype(np.uint8)
+    _check(dev, oracle, lut, u8, k, id_offset=7)

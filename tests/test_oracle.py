@@ -189,3 +189,17 @@ def test_rabitq_estimator_restatement_matches_fp64_formula():
     ip = O.rabitq_est(codes_ip, d, Q, c, qb=0, metric=0)
     np.testing.assert_allclose(ip, want_ip, rtol=1e-4, atol=1e-3)
     assert np.corrcoef(ip.ravel(), -(Q @ X.T).ravel())[0, 1] > 0.6  # 1-bit codes, d = 64
+
+
+def test_oracle_asan_selftest():
+    """the CPU oracle under -fsanitize=address,undefined (oracle/selftest.c runs
+    every exported restatement at the shape edges; `make -C oracle asan` builds and runs it)."""
+    import shutil
+    from pathlib import Path
+    import subprocess
+
+    if shutil.which("gcc") is None and shutil.which("cc") is None:
+        pytest.skip("no C compiler")
+    p = subprocess.run(["make", "-s", "-C", str(Path(__file__).resolve().parents[1] / "oracle"), "asan"], capture_output=True, text=True, timeout=300)
+    assert p.returncode == 0, p.stdout[-3000:] + p.stderr[-3000:]
+    assert "oracle selftest ok" in p.stdout

@@ -121,6 +121,8 @@ __device__ __forceinline__ void lut_add(const float* tab, uint32_t mk, float (&d
 
 typedef float f32x4v __attribute__((ext_vector_type(4)));
 typedef __attribute__((address_space(3))) const f32x4v lds_f4;
+typedef unsigned int u32x4v __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(3))) const u32x4v lds_u4;
 
 // Undoes the odd lanes' half order of lut_add<8> (identity for other QB).
 template <int QB>
@@ -144,23 +146,31 @@ template <int R, int QB, int MC>
 __global__ __launch_bounds__(kScanWaves * 64) void adc_scan_kernel(
     const float* __restrict__ lut, int64_t nq, const uint8_t* __restrict__ codes, int64_t n, int M,
     int ksub, int k, int64_t id_offset, int64_t chunk_rows, float* __restrict__ part_d,
-    uint32_t* __restrict__ part_i) {
+    uint32_t* __restrict__ part_i, const int* __restrict__ qlist, const int* __restrict__ qcount) {
     if constexpr (MC > 0) {
         M = 16 * MC;
         ksub = 256;
     }
+    // qlist (the exact re-run of queries the filtered search could not certify, below): query
+    // slot s of this launch is query qlist[s], s < *qcount; the lists are written per slot
     // [M][ksub][QB]: the QB queries' entries of one (m, code) are adjacent, so one 16-B LDS
     // read serves 4 queries (random codes: ~2x fewer bank-conflict cycles per lookup than
     // QB separate 4-B reads)
     extern __shared__ __attribute__((aligned(16))) float tab[];
     const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
     const int64_t q0 = (int64_t)blockIdx.y * QB;
-    const int nqb = (int)min<int64_t>(QB, nq - q0);
+    int nqb = (int)min<int64_t>(QB, nq - q0);
+    if (qlist != nullptr) {
+        const int cnt = *qcount;
+        if (q0 >= cnt) return;  // whole workgroup, before any barrier
+        nqb = (int)min<int64_t>(QB, cnt - q0);
+    }
     const int64_t tab_elems = (int64_t)M * ksub;
     for (int64_t e = tid; e < tab_elems * QB; e += kScanWaves * 64) {
         const int64_t mk = e / QB;
         const int qq = (int)(e - mk * QB);
-        tab[e] = qq < nqb ? lut[(q0 + qq) * tab_elems + mk] : 0.0f;
+        const int64_t qsrc = qq < nqb ? (qlist != nullptr ? (int64_t)qlist[q0 + qq] : q0 + qq) : 0;
+        tab[e] = qq < nqb ? lut[qsrc * tab_elems + mk] : 0.0f;
     }
     __syncthreads();
 
@@ -375,13 +385,14 @@ __global__ __launch_bounds__(kScanWaves * 64) void flat_scan_kernel(
     const int64_t part = (int64_t)blockIdx.x * kScanWaves + wv;
 #pragma unroll
     for (int qq = 0; qq < QB; ++qq) {
-        if (qq >= nqb) break;
-        float* od = part_d + (part * nq + q0 + qq) * k;
-        uint32_t* oi = part_i + (part * nq + q0 + qq) * k;
+        if (qq < nqb) {
+            float* od = part_d + (part * nq + q0 + qq) * k;
+            uint32_t* oi = part_i + (part * nq + q0 + qq) * k;
 #pragma unroll
-        for (int r = 0; r < R; ++r) {
-            const int e = r * 64 + lane;
-            if (e < k) { od[e] = top[qq].d[r]; oi[e] = top[qq].id[r]; }
+            for (int r = 0; r < R; ++r) {
+                const int e = r * 64 + lane;
+                if (e < k) { od[e] = top[qq].d[r]; oi[e] = top[qq].id[r]; }
+            }
         }
     }
 }
@@ -391,10 +402,13 @@ __global__ __launch_bounds__(kScanWaves * 64) void flat_scan_kernel(
 template <int R>
 __global__ __launch_bounds__(256) void topk_merge_kernel(const float* __restrict__ in_d, const uint32_t* __restrict__ in_i,
                                                          int parts, int64_t nq, int k, float* __restrict__ out_d,
-                                                         uint32_t* __restrict__ out_i) {
+                                                         uint32_t* __restrict__ out_i, const int* __restrict__ qlist,
+                                                         const int* __restrict__ qcount) {
     const int lane = threadIdx.x & 63;
     const int64_t qi = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
     if (qi >= nq) return;  // whole wave
+    if (qlist != nullptr && qi >= *qcount) return;
+    const int64_t qo = qlist != nullptr ? (int64_t)qlist[qi] : qi;  // output row of list slot qi
     WaveTopK<R> top;
     top.init();
     float thr_d = INFINITY;
@@ -425,7 +439,333 @@ __global__ __launch_bounds__(256) void topk_merge_kernel(const float* __restrict
 #pragma unroll
     for (int r = 0; r < R; ++r) {
         const int e = r * 64 + lane;
-        if (e < k) { out_d[qi * k + e] = top.d[r]; out_i[qi * k + e] = top.id[r]; }
+        if (e < k) { out_d[qo * k + e] = top.d[r]; out_i[qo * k + e] = top.id[r]; }
+    }
+}
+
+// ---------------------------------------------------------------------------------------------
+// Filtered ADC search (M = 16 / 32, ksub = 256): the same canonical fp32 top-k, found in two
+// passes.
+//
+// 1. adc_qstats_kernel / adc_qtab_kernel quantise every query's LUT to integers:
+//      q[m][c] = min(QMAX, floor((lut[m][c] - min_m) / delta)),  delta = max_m range_m / QMAX,
+//    QMAX = floor(32767 / M), so a row's sum S = sum_m q[m][code_m] <= 32767 (15 bits).  Two
+//    queries share a dword (16-bit fields), 16 (M = 16) or 8 (M = 32) queries one 32 / 16-B
+//    table entry: half the LDS bytes and VALU adds per (query, row) of the fp32 table, and the
+//    adds are plain v_add_u32 (no carry can cross a field: every partial sum < 2^15).
+// 2. adc_qscan_kernel keeps, per part (workgroup chunk x wave) and query, the exact top-k of
+//    (S, id): a screen of all queries at once (SWAR: field (0x8000 + t) - S has bit 15 set iff
+//    S <= t, no borrow since S, t < 2^15) and the same wave-resident lists as the fp32 scan.
+// 3. adc_rerank_kernel (one wave per query) evaluates the canonical fp32 distance (the sum over
+//    m in order of the fp32 LUT entries, include/mivq.h) of every listed row and keeps the exact
+//    top-k.  It is the canonical answer if no row outside the lists can beat its k-th element
+//    (E_k): a row missing from part p's full list has S >= S_k(p), and, with q*delta <=
+//    lut - min, its canonical distance is >= LB(S) = base + delta * S - margin (base = sum_m
+//    min_m, margin >= the fp32 summation error gamma_M * sum_m max_c |lut[m][c]| plus fp64
+//    slack).  So the query is certified when LB(S_k(p)) > E_k for every part p whose list is
+//    full; a query that is not (or whose LUT is not finite) is listed for
+// 4. the fp32 scan (adc_scan_kernel) re-run on the listed queries only (query indirection; the
+//    workgroups of empty slots return at once) and its merge.
+// Results are identical to the fp32 scan's for every input.
+struct AdcQStat {
+    double base, delta, margin;
+    int bad, pad;
+};
+
+__host__ __device__ constexpr int adc_qmax(int M) { return 32767 / M; }
+
+__device__ __forceinline__ float wave_min(float v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v = fminf(v, __shfl_xor(v, o));
+    return v;
+}
+__device__ __forceinline__ float wave_max(float v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o));
+    return v;
+}
+
+// grid nq, block 256: per (query, m) the minimum and range (mins[q][m] = min_m), then the
+// query's {base, delta, margin, bad}.
+__global__ __launch_bounds__(256) void adc_qstats_kernel(const float* __restrict__ lut, int64_t nq, int M,
+                                                         float* __restrict__ mins, AdcQStat* __restrict__ qs) {
+    __shared__ double s_min[64], s_rng[64], s_abs[64];
+    __shared__ int s_bad;
+    const int64_t qi = blockIdx.x;
+    const int w = threadIdx.x >> 6, l = threadIdx.x & 63;
+    if (threadIdx.x == 0) s_bad = 0;
+    __syncthreads();
+    for (int m = w; m < M; m += 4) {
+        const float4 v = *reinterpret_cast<const float4*>(lut + (qi * M + m) * 256 + 4 * l);
+        const bool fin = isfinite(v.x) && isfinite(v.y) && isfinite(v.z) && isfinite(v.w);
+        const float mn = wave_min(fminf(fminf(v.x, v.y), fminf(v.z, v.w)));
+        const float mx = wave_max(fmaxf(fmaxf(v.x, v.y), fmaxf(v.z, v.w)));
+        const float ab = wave_max(fmaxf(fmaxf(fabsf(v.x), fabsf(v.y)), fmaxf(fabsf(v.z), fabsf(v.w))));
+        const bool bad = __ballot(!fin) != 0ull;
+        if (l == 0) {
+            s_min[m] = mn;
+            s_rng[m] = (double)mx - (double)mn;
+            s_abs[m] = ab;
+            mins[qi * M + m] = mn;
+            if (bad) s_bad = 1;
+        }
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        double base = 0.0, rng = 0.0, mag = 0.0;
+        for (int m = 0; m < M; ++m) {
+            base += s_min[m];
+            rng = fmax(rng, s_rng[m]);
+            mag += s_abs[m];
+        }
+        AdcQStat st;
+        st.base = base;
+        st.delta = rng > 0.0 ? rng / (double)adc_qmax(M) : 1.0;
+        // fp32 canonical sum: |fl(sum) - sum| <= gamma_{M-1} sum |t| <= gamma_M mag; 2x that, plus
+        // fp64 slack for base and delta * S
+        st.margin = 2.0 * (double)M * 5.9604644775390625e-8 * mag + 1e-12 * (mag + fabs(base));
+        st.bad = s_bad || !isfinite(base) || !isfinite(mag) || !(st.delta > 0.0);
+        st.pad = 0;
+        qs[qi] = st;
+    }
+}
+
+// grid (ceil(nq / QB), M), block 256 (code c): table block b = (M, 256, QB / 2) dwords, query
+// 2j in the low and 2j + 1 in the high half of dword j.  q <= (lut - min) / delta (the ratio
+// is shrunk by 2^-50 before the floor, so fp64 rounding never rounds it up past an integer).
+template <int QB>
+__global__ __launch_bounds__(256) void adc_qtab_kernel(const float* __restrict__ lut, int64_t nq, int M,
+                                                       const float* __restrict__ mins,
+                                                       const AdcQStat* __restrict__ qs, uint32_t* __restrict__ tab) {
+    const int64_t qb = blockIdx.x;
+    const int m = blockIdx.y, c = threadIdx.x;
+    const int qmax = adc_qmax(M);
+    uint32_t w[QB / 2];
+#pragma unroll
+    for (int j = 0; j < QB / 2; ++j) w[j] = 0u;
+#pragma unroll
+    for (int qq = 0; qq < QB; ++qq) {
+        const int64_t qi = qb * QB + qq;
+        uint32_t v = 0u;
+        if (qi < nq) {
+            const AdcQStat st = qs[qi];
+            if (!st.bad) {
+                const double x = ((double)lut[(qi * M + m) * 256 + c] - (double)mins[qi * M + m]) / st.delta *
+                                 (1.0 - 8.881784197001252e-16);
+                v = x >= (double)qmax ? (uint32_t)qmax : x > 0.0 ? (uint32_t)floor(x) : 0u;
+            }
+        }
+        w[qq >> 1] |= v << (16 * (qq & 1));
+    }
+    uint32_t* dst = tab + ((qb * M + m) * 256 + c) * (QB / 2);
+#pragma unroll
+    for (int j = 0; j < QB / 2; j += 4) *reinterpret_cast<uint4*>(dst + j) = make_uint4(w[j], w[j + 1], w[j + 2], w[j + 3]);
+}
+
+// grid (nchunks, ceil(nq / QB)), block kScanWaves waves (the fp32 scan's structure): the
+// integer tables of QB queries in LDS, M = 16 MC, each lane one row per wave-step with its
+// code row loaded a step ahead.  Part lists of (float(S), id), k per query.
+template <int R, int QB, int MC>
+__global__ __launch_bounds__(kScanWaves * 64) void adc_qscan_kernel(
+    const uint32_t* __restrict__ qtab, int64_t nq, const uint8_t* __restrict__ codes, int64_t n, int k,
+    int64_t id_offset, int64_t chunk_rows, float* __restrict__ part_d, uint32_t* __restrict__ part_i) {
+    constexpr int M = 16 * MC;
+    constexpr int NWD = QB / 2;  // dwords per (m, code) entry
+    extern __shared__ __attribute__((aligned(16))) uint32_t qt[];  // [M][256][NWD]
+    const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+    const int64_t q0 = (int64_t)blockIdx.y * QB;
+    const int nqb = (int)min<int64_t>(QB, nq - q0);
+    {
+        const uint4* src = reinterpret_cast<const uint4*>(qtab + (int64_t)blockIdx.y * M * 256 * NWD);
+        uint4* dst = reinterpret_cast<uint4*>(qt);
+        for (int e = tid; e < M * 256 * NWD / 4; e += kScanWaves * 64) dst[e] = src[e];
+    }
+    __syncthreads();
+
+    WaveTopK<R> top[QB];
+    float thr_d[QB];
+    uint32_t thr_i[QB];
+#pragma unroll
+    for (int qq = 0; qq < QB; ++qq) {
+        top[qq].init();
+        thr_d[qq] = INFINITY;
+        thr_i[qq] = kNoId;
+    }
+    // screen words: field j of query pair (2j, 2j+1) holds min(threshold, 0x7FFF) | 0x8000
+    uint32_t tw[NWD];
+#pragma unroll
+    for (int j = 0; j < NWD; ++j) tw[j] = 0xFFFFFFFFu;
+
+    const int64_t rbeg = (int64_t)blockIdx.x * chunk_rows;
+    const int64_t rend = min(n, rbeg + chunk_rows);
+    const uint32_t par = (uint32_t)lane & 1u;
+    const uint32_t tbase = (uint32_t)(uintptr_t)qt + (NWD == 8 ? 16u * par : 0u);
+    uint4 cw[MC];
+    auto fetch = [&](int64_t row) __attribute__((always_inline)) {
+        const uint4* cr = reinterpret_cast<const uint4*>(codes + row * (16 * MC));
+#pragma unroll
+        for (int c = 0; c < MC; ++c) cw[c] = row < rend ? cr[c] : make_uint4(0u, 0u, 0u, 0u);
+    };
+    fetch(rbeg + (int64_t)wv * 64 + lane);
+    for (int64_t base = rbeg + (int64_t)wv * 64; base < rend; base += kScanWaves * 64) {
+        const int64_t row = base + lane;
+        const bool valid = row < rend;
+        uint32_t acc[NWD];
+#pragma unroll
+        for (int j = 0; j < NWD; ++j) acc[j] = 0u;
+        uint4 cur[MC];
+#pragma unroll
+        for (int c = 0; c < MC; ++c) cur[c] = cw[c];
+        fetch(row + kScanWaves * 64);
+        uint32_t wq[4 * MC];
+#pragma unroll
+        for (int c = 0; c < MC; ++c) {
+            wq[4 * c + 0] = cur[c].x; wq[4 * c + 1] = cur[c].y;
+            wq[4 * c + 2] = cur[c].z; wq[4 * c + 3] = cur[c].w;
+        }
+#pragma unroll 1
+        for (int jw = 0; jw < 4 * MC; ++jw) {
+            const uint32_t wrd = wq[0];
+            const uint32_t wofs = tbase + (uint32_t)jw * (4u * 256u * 4u * NWD);
+#pragma unroll
+            for (int b = 0; b < 4; ++b) {
+                uint32_t cb, o1;
+                asm("v_bfe_u32 %0, %1, %2, 8" : "=v"(cb) : "v"(wrd), "i"(8 * b));
+                if constexpr (NWD == 8) {
+                    // 32-B entries as two 16-B halves, odd lanes in the opposite order (two 8-into-8
+                    // bank draws per 16-lane group, as the fp32 scan); integer sums do not care
+                    uint32_t o2;
+                    asm("v_lshl_add_u32 %0, %1, 5, %2" : "=v"(o1) : "v"(cb), "v"(wofs));
+                    asm("v_xor_b32 %0, 16, %1" : "=v"(o2) : "v"(o1));
+                    const u32x4v t0 = *(reinterpret_cast<const lds_u4*>((uintptr_t)o1) + b * 512);
+                    const u32x4v t1 = *(reinterpret_cast<const lds_u4*>((uintptr_t)o2) + b * 512);
+                    acc[0] += t0.x; acc[1] += t0.y; acc[2] += t0.z; acc[3] += t0.w;
+                    acc[4] += t1.x; acc[5] += t1.y; acc[6] += t1.z; acc[7] += t1.w;
+                } else {
+                    asm("v_lshl_add_u32 %0, %1, 4, %2" : "=v"(o1) : "v"(cb), "v"(wofs));
+                    const u32x4v t0 = *(reinterpret_cast<const lds_u4*>((uintptr_t)o1) + b * 256);
+                    acc[0] += t0.x; acc[1] += t0.y; acc[2] += t0.z; acc[3] += t0.w;
+                }
+            }
+#pragma unroll
+            for (int t = 0; t + 1 < 4 * MC; ++t) wq[t] = wq[t + 1];
+        }
+        if constexpr (NWD == 8) {  // odd lanes hold the second half first
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                const uint32_t a = acc[j], b2 = acc[j + 4];
+                acc[j] = par ? b2 : a;
+                acc[j + 4] = par ? a : b2;
+            }
+        }
+        uint32_t hit = 0u;
+#pragma unroll
+        for (int j = 0; j < NWD; ++j) hit |= (tw[j] - acc[j]) & 0x80008000u;
+        if (__ballot(valid && hit != 0u) == 0ull) continue;  // the common case: nothing to insert
+        const uint32_t gid = (uint32_t)(id_offset + row);
+#pragma unroll
+        for (int j = 0; j < NWD; ++j) {
+            // only the pairs whose screen fired (wave-uniform test)
+            if (__ballot(valid && ((tw[j] - acc[j]) & 0x80008000u) != 0u) == 0ull) continue;
+            uint32_t tnew = 0u;
+#pragma unroll
+            for (int h = 0; h < 2; ++h) {
+                const int qq = 2 * j + h;
+                if (qq < nqb) {
+                    const float key = (float)((acc[j] >> (16 * h)) & 0xFFFFu);
+                    top[qq].offer(valid, key, gid, k, lane, thr_d[qq], thr_i[qq]);
+                }
+                const uint32_t t = thr_d[qq] < 32767.0f ? (uint32_t)thr_d[qq] : 0x7FFFu;
+                tnew |= (t | 0x8000u) << (16 * h);
+            }
+            tw[j] = tnew;
+        }
+    }
+    const int64_t part = (int64_t)blockIdx.x * kScanWaves + wv;
+#pragma unroll
+    for (int qq = 0; qq < QB; ++qq) {
+        if (qq < nqb) {
+            float* od = part_d + (part * nq + q0 + qq) * k;
+            uint32_t* oi = part_i + (part * nq + q0 + qq) * k;
+#pragma unroll
+            for (int r = 0; r < R; ++r) {
+                const int e = r * 64 + lane;
+                if (e < k) { od[e] = top[qq].d[r]; oi[e] = top[qq].id[r]; }
+            }
+        }
+    }
+}
+
+// One wave per query: canonical fp32 distances of the listed rows, exact top-k, certificate.
+template <int R, int MC>
+__global__ __launch_bounds__(256) void adc_rerank_kernel(const float* __restrict__ lut, int64_t nq,
+                                                         const uint8_t* __restrict__ codes, int64_t id_offset,
+                                                         const float* __restrict__ pd, const uint32_t* __restrict__ pi,
+                                                         int parts, int k, const AdcQStat* __restrict__ qs,
+                                                         float* __restrict__ out_d, uint32_t* __restrict__ out_i,
+                                                         int* __restrict__ fail_list, int* __restrict__ fail_count) {
+    constexpr int M = 16 * MC;
+    const int lane = threadIdx.x & 63;
+    const int64_t qi = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (qi >= nq) return;  // whole wave
+    const AdcQStat st = qs[qi];
+    WaveTopK<R> top;
+    top.init();
+    float thr_d = INFINITY;
+    uint32_t thr_i = kNoId;
+    const float* lq = lut + qi * M * 256;
+    const int64_t total = (int64_t)parts * k;
+    for (int64_t e0 = 0; e0 < total; e0 += 64) {
+        const int64_t e = e0 + lane;
+        uint32_t id = kNoId;
+        if (e < total) {
+            const int64_t p = e / k, j = e - p * k;
+            id = pi[(p * nq + qi) * k + j];
+        }
+        const bool valid = id != kNoId;
+        float dv = INFINITY;
+        if (valid) {
+            const uint4* cr = reinterpret_cast<const uint4*>(codes + ((int64_t)id - id_offset) * M);
+            uint4 cw[MC];
+#pragma unroll
+            for (int c = 0; c < MC; ++c) cw[c] = cr[c];
+            float t[M];
+#pragma unroll
+            for (int c = 0; c < MC; ++c) {
+                const uint32_t wd[4] = {cw[c].x, cw[c].y, cw[c].z, cw[c].w};
+#pragma unroll
+                for (int j = 0; j < 16; ++j)
+                    t[16 * c + j] = lq[(16 * c + j) * 256 + ((wd[j >> 2] >> (8 * (j & 3))) & 0xFFu)];
+            }
+            dv = 0.0f;
+#pragma unroll
+            for (int m = 0; m < M; ++m) dv += t[m];  // the canonical order
+            if (dv != dv) dv = INFINITY;
+        }
+        top.offer(valid, dv, id, k, lane, thr_d, thr_i);
+    }
+    // certificate: every full part list's k-th S must bound its missing rows above E_k
+    bool ok = !st.bad;
+    for (int p0 = 0; p0 < parts; p0 += 64) {
+        const int p = p0 + lane;
+        bool f = false;
+        if (p < parts) {
+            const int64_t at = ((int64_t)p * nq + qi) * k + (k - 1);
+            if (pi[at] != kNoId) {
+                const double lb = st.base + st.delta * (double)pd[at] - st.margin;
+                f = !(lb > (double)thr_d);
+            }
+        }
+        if (__ballot(f) != 0ull) ok = false;
+    }
+    if (ok) {
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+            const int e = r * 64 + lane;
+            if (e < k) { out_d[qi * k + e] = top.d[r]; out_i[qi * k + e] = top.id[r]; }
+        }
+    } else if (lane == 0) {
+        fail_list[atomicAdd(fail_count, 1)] = (int)qi;
     }
 }
 
@@ -460,7 +800,8 @@ int64_t adc_chunks(int64_t nq, int64_t n, int QB) {
 
 template <int R, int QB>
 hipError_t launch_scan(const float* lut, int64_t nq, const uint8_t* codes, int64_t n, int M, int ksub, int k,
-                       int64_t id_offset, int64_t nch, float* pd, uint32_t* pi, hipStream_t st) {
+                       int64_t id_offset, int64_t nch, float* pd, uint32_t* pi, hipStream_t st,
+                       const int* qlist = nullptr, const int* qcount = nullptr) {
     const size_t smem = (size_t)QB * M * ksub * sizeof(float);
     const bool vec = ksub == 256 && reinterpret_cast<uintptr_t>(codes) % 16 == 0;
     auto kern = vec && M == 16 ? adc_scan_kernel<R, QB, 1> : vec && M == 32 ? adc_scan_kernel<R, QB, 2>
@@ -469,18 +810,19 @@ hipError_t launch_scan(const float* lut, int64_t nq, const uint8_t* codes, int64
     if (e != hipSuccess) return e;
     const int64_t chunk_rows = ceil_div(n, nch);
     hipLaunchKernelGGL(kern, dim3((unsigned)nch, (unsigned)ceil_div(nq, QB)), dim3(kScanWaves * 64), smem, st, lut, nq, codes,
-                       n, M, ksub, k, id_offset, chunk_rows, pd, pi);
+                       n, M, ksub, k, id_offset, chunk_rows, pd, pi, qlist, qcount);
     return hipGetLastError();
 }
 
 template <int R>
 hipError_t launch_scan_r(int QB, const float* lut, int64_t nq, const uint8_t* codes, int64_t n, int M, int ksub,
-                         int k, int64_t id_offset, int64_t nch, float* pd, uint32_t* pi, hipStream_t st) {
+                         int k, int64_t id_offset, int64_t nch, float* pd, uint32_t* pi, hipStream_t st,
+                         const int* qlist = nullptr, const int* qcount = nullptr) {
     switch (QB) {
-        case 8: return launch_scan<R, 8>(lut, nq, codes, n, M, ksub, k, id_offset, nch, pd, pi, st);
-        case 4: return launch_scan<R, 4>(lut, nq, codes, n, M, ksub, k, id_offset, nch, pd, pi, st);
-        case 2: return launch_scan<R, 2>(lut, nq, codes, n, M, ksub, k, id_offset, nch, pd, pi, st);
-        default: return launch_scan<R, 1>(lut, nq, codes, n, M, ksub, k, id_offset, nch, pd, pi, st);
+        case 8: return launch_scan<R, 8>(lut, nq, codes, n, M, ksub, k, id_offset, nch, pd, pi, st, qlist, qcount);
+        case 4: return launch_scan<R, 4>(lut, nq, codes, n, M, ksub, k, id_offset, nch, pd, pi, st, qlist, qcount);
+        case 2: return launch_scan<R, 2>(lut, nq, codes, n, M, ksub, k, id_offset, nch, pd, pi, st, qlist, qcount);
+        default: return launch_scan<R, 1>(lut, nq, codes, n, M, ksub, k, id_offset, nch, pd, pi, st, qlist, qcount);
     }
 }
 
@@ -516,16 +858,86 @@ hipError_t launch_flat_r(int QB, const float* q, int64_t nq, const float* x, int
     }
 }
 
+// Filtered path eligibility by shape (the workspace is sized on shape alone) and the profiling
+// switch MIVQ_ADC_EXACT=1 (the fp32 scan for every query).
+// (queries per table block: the variants whose lists fit the 128 registers of the 16-wave scan)
+bool adc_filtered_shape(int M, int ksub, int k) {
+    return ksub == 256 && (M == 16 || (M == 32 && k <= 192)) && k <= 256;
+}
+int adc_fqb(int M, int k) { return M == 16 && k <= 64 ? 16 : 8; }
+
+struct AdcFilteredLayout {
+    size_t stats, mins, tab, p1d, p1i, fail, total;
+    int64_t nch, parts;
+};
+
+AdcFilteredLayout adc_filtered_layout(int64_t nq, int64_t n, int M, int k, size_t off) {
+    AdcFilteredLayout L{};
+    const int QB = adc_fqb(M, k);
+    L.nch = adc_chunks(nq, n, QB);
+    L.parts = L.nch * kScanWaves;
+    L.stats = off;  off = align_up(off + (size_t)nq * sizeof(AdcQStat), 256);
+    L.mins = off;   off = align_up(off + (size_t)nq * M * sizeof(float), 256);
+    L.tab = off;    off = align_up(off + (size_t)ceil_div(nq, QB) * M * 256 * (QB / 2) * sizeof(uint32_t), 256);
+    L.p1d = off;    off = align_up(off + (size_t)L.parts * nq * k * sizeof(float), 256);
+    L.p1i = off;    off = align_up(off + (size_t)L.parts * nq * k * sizeof(uint32_t), 256);
+    L.fail = off;   off = align_up(off + (size_t)(nq + 1) * sizeof(int), 256);
+    L.total = off;
+    return L;
+}
+
+template <int R, int MC, int QB>
+hipError_t launch_filtered_r(const float* lut, int64_t nq, const uint8_t* codes, int64_t n, int k, int64_t id_offset,
+                             unsigned char* ws, const AdcFilteredLayout& L, float* dists, uint32_t* ids,
+                             hipStream_t st) {
+    constexpr int M = 16 * MC;
+    auto* qs = reinterpret_cast<AdcQStat*>(ws + L.stats);
+    auto* mins = reinterpret_cast<float*>(ws + L.mins);
+    auto* tab = reinterpret_cast<uint32_t*>(ws + L.tab);
+    auto* p1d = reinterpret_cast<float*>(ws + L.p1d);
+    auto* p1i = reinterpret_cast<uint32_t*>(ws + L.p1i);
+    int* fail_count = reinterpret_cast<int*>(ws + L.fail);
+    int* fail_list = fail_count + 1;
+    hipError_t e = hipMemsetAsync(fail_count, 0, sizeof(int), st);
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(adc_qstats_kernel, dim3((unsigned)nq), dim3(256), 0, st, lut, nq, M, mins, qs);
+    const int64_t qblocks = ceil_div(nq, QB);
+    hipLaunchKernelGGL(adc_qtab_kernel<QB>, dim3((unsigned)qblocks, (unsigned)M), dim3(256), 0, st, lut, nq, M, mins, qs,
+                       tab);
+    auto kern = adc_qscan_kernel<R, QB, MC>;
+    const int smem = M * 256 * QB * 2;
+    e = hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, smem);
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(kern, dim3((unsigned)L.nch, (unsigned)qblocks), dim3(kScanWaves * 64), smem, st, tab, nq, codes, n,
+                       k, id_offset, ceil_div(n, L.nch), p1d, p1i);
+    hipLaunchKernelGGL((adc_rerank_kernel<R, MC>), dim3((unsigned)ceil_div(nq, 4)), dim3(256), 0, st, lut, nq, codes,
+                       id_offset, p1d, p1i, (int)L.parts, k, qs, dists, ids, fail_list, fail_count);
+    return hipGetLastError();
+}
+
+hipError_t launch_filtered(int M, const float* lut, int64_t nq, const uint8_t* codes, int64_t n, int k,
+                           int64_t id_offset, unsigned char* ws, const AdcFilteredLayout& L, float* dists,
+                           uint32_t* ids, hipStream_t st) {
+    const int R = (k + 63) / 64;
+#define MIVQ_F(RR, MCC, QBB) \
+    return launch_filtered_r<RR, MCC, QBB>(lut, nq, codes, n, k, id_offset, ws, L, dists, ids, st)
+    if (M == 16) {
+        switch (R) { case 1: MIVQ_F(1, 1, 16); case 2: MIVQ_F(2, 1, 8); case 3: MIVQ_F(3, 1, 8); default: MIVQ_F(4, 1, 8); }
+    }
+    switch (R) { case 1: MIVQ_F(1, 2, 8); case 2: MIVQ_F(2, 2, 8); default: MIVQ_F(3, 2, 8); }
+#undef MIVQ_F
+}
+
 }  // namespace
 
 hipError_t launch_topk_merge(const float* pd, const uint32_t* pi, int parts, int64_t nq, int k, float* od, uint32_t* oi,
-                        hipStream_t st) {
+                        hipStream_t st, const int* qlist, const int* qcount) {
     const dim3 grid((unsigned)ceil_div(nq, 4)), block(256);
     switch ((k + 63) / 64) {
-        case 1: hipLaunchKernelGGL(topk_merge_kernel<1>, grid, block, 0, st, pd, pi, parts, nq, k, od, oi); break;
-        case 2: hipLaunchKernelGGL(topk_merge_kernel<2>, grid, block, 0, st, pd, pi, parts, nq, k, od, oi); break;
-        case 3: hipLaunchKernelGGL(topk_merge_kernel<3>, grid, block, 0, st, pd, pi, parts, nq, k, od, oi); break;
-        default: hipLaunchKernelGGL(topk_merge_kernel<4>, grid, block, 0, st, pd, pi, parts, nq, k, od, oi); break;
+        case 1: hipLaunchKernelGGL(topk_merge_kernel<1>, grid, block, 0, st, pd, pi, parts, nq, k, od, oi, qlist, qcount); break;
+        case 2: hipLaunchKernelGGL(topk_merge_kernel<2>, grid, block, 0, st, pd, pi, parts, nq, k, od, oi, qlist, qcount); break;
+        case 3: hipLaunchKernelGGL(topk_merge_kernel<3>, grid, block, 0, st, pd, pi, parts, nq, k, od, oi, qlist, qcount); break;
+        default: hipLaunchKernelGGL(topk_merge_kernel<4>, grid, block, 0, st, pd, pi, parts, nq, k, od, oi, qlist, qcount); break;
     }
     return hipGetLastError();
 }
@@ -615,7 +1027,11 @@ extern "C" size_t mivq_adc_search_workspace_bytes(int64_t nq, int64_t n, int32_t
     const int QB = adc_qb(M, 1 << nbits);
     if (QB == 0) return 0;
     const int64_t parts = adc_chunks(nq, n, QB) * kScanWaves;
-    return align_up((size_t)parts * nq * k * sizeof(float), 256) + align_up((size_t)parts * nq * k * 4, 256);
+    // the fp32 scan's part lists (every query, or the filtered path's uncertified ones) ...
+    const size_t exact = align_up((size_t)parts * nq * k * sizeof(float), 256) + align_up((size_t)parts * nq * k * 4, 256);
+    // ... then the filtered path's regions
+    if (!adc_filtered_shape(M, 1 << nbits, k)) return exact;
+    return adc_filtered_layout(nq, n, M, k, exact).total;
 }
 
 extern "C" int mivq_adc_search(const float* lut, int64_t nq, const uint8_t* codes, int64_t n, int32_t M,
@@ -646,18 +1062,36 @@ extern "C" int mivq_adc_search(const float* lut, int64_t nq, const uint8_t* code
     const int64_t nch = adc_chunks(nq, n, QB);
     const int parts = (int)(nch * kScanWaves);
     float* pd = static_cast<float*>(workspace);
+    const size_t exact_bytes = align_up((size_t)parts * nq * k * sizeof(float), 256) + align_up((size_t)parts * nq * k * 4, 256);
     uint32_t* pi = reinterpret_cast<uint32_t*>(static_cast<unsigned char*>(workspace) +
                                                align_up((size_t)parts * nq * k * sizeof(float), 256));
-    const int R = (k + 63) / 64;
+    // the filtered path (integer-LUT scan + exact re-rank + certificate; the fp32 scan re-runs
+    // only the uncertified queries): same results, ~half the LDS traffic per (query, row)
+    const char* force_exact = getenv("MIVQ_ADC_EXACT");  // profiling: the fp32 scan for every query
+    const bool filtered = adc_filtered_shape(M, ksub, k) && reinterpret_cast<uintptr_t>(codes) % 16 == 0 &&
+                          reinterpret_cast<uintptr_t>(lut) % 16 == 0 && !(force_exact && atoi(force_exact) != 0);
+    const int* qlist = nullptr;
+    const int* qcount = nullptr;
     hipError_t e;
+    if (filtered) {
+        const AdcFilteredLayout FL = adc_filtered_layout(nq, n, M, k, exact_bytes);
+        unsigned char* ws = static_cast<unsigned char*>(workspace);
+        e = launch_filtered(M, lut, nq, codes, n, k, id_offset, ws, FL, dists, ids, st);
+        if (e != hipSuccess) return set_error(MIVQ_ERR_HIP, "adc_search (filtered): %s", hipGetErrorString(e));
+        qcount = reinterpret_cast<const int*>(ws + FL.fail);
+        qlist = qcount + 1;
+        const char* nofb = getenv("MIVQ_ADC_NO_FALLBACK");  // tests: certified queries only (others unset)
+        if (nofb && atoi(nofb) != 0) return MIVQ_OK;
+    }
+    const int R = (k + 63) / 64;
     switch (R) {
-        case 1: e = launch_scan_r<1>(QB, lut, nq, codes, n, M, ksub, k, id_offset, nch, pd, pi, st); break;
-        case 2: e = launch_scan_r<2>(QB, lut, nq, codes, n, M, ksub, k, id_offset, nch, pd, pi, st); break;
-        case 3: e = launch_scan_r<3>(QB, lut, nq, codes, n, M, ksub, k, id_offset, nch, pd, pi, st); break;
-        default: e = launch_scan_r<4>(QB, lut, nq, codes, n, M, ksub, k, id_offset, nch, pd, pi, st); break;
+        case 1: e = launch_scan_r<1>(QB, lut, nq, codes, n, M, ksub, k, id_offset, nch, pd, pi, st, qlist, qcount); break;
+        case 2: e = launch_scan_r<2>(QB, lut, nq, codes, n, M, ksub, k, id_offset, nch, pd, pi, st, qlist, qcount); break;
+        case 3: e = launch_scan_r<3>(QB, lut, nq, codes, n, M, ksub, k, id_offset, nch, pd, pi, st, qlist, qcount); break;
+        default: e = launch_scan_r<4>(QB, lut, nq, codes, n, M, ksub, k, id_offset, nch, pd, pi, st, qlist, qcount); break;
     }
     if (e != hipSuccess) return set_error(MIVQ_ERR_HIP, "adc_scan: %s", hipGetErrorString(e));
-    e = launch_topk_merge(pd, pi, parts, nq, k, dists, ids, st);
+    e = launch_topk_merge(pd, pi, parts, nq, k, dists, ids, st, qlist, qcount);
     if (e != hipSuccess) return set_error(MIVQ_ERR_HIP, "topk_merge: %s", hipGetErrorString(e));
     return MIVQ_OK;
 }

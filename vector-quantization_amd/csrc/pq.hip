@@ -798,9 +798,6 @@ extern "C" size_t mivq_pq_encode_workspace_bytes(int64_t n, int32_t d, int32_t M
     // cs path: n*M uint2 resolve items; legacy MFMA path: its filter flags (never both)
     b += align_up(std::max((size_t)n * M * 8, (size_t)ceil_div(n, 32) * M * sizeof(uint32_t)), 256);
     b += align_up(cs_counts_bytes(n, M), 256);  // cs path: list counts per workgroup
-#ifdef MIVQ_CS_TIMESTAMPS
-    b += align_up((size_t)n * M * 8, 256);      // probe build: per-workgroup timestamps
-#endif
     return b;
 }
 
@@ -833,13 +830,6 @@ extern "C" int mivq_pq_encode(const float* x, int64_t n, int32_t d, int32_t M, i
     off += align_up(std::max((size_t)n * M * 8, (size_t)ceil_div(n, 32) * M * sizeof(uint32_t)), 256);
     void* counts = ws + off;
     off += align_up(cs_counts_bytes(n, M), 256);
-    // {score gap, Xs} per pair item feed only the round-1 pair kernel (profiling builds); the
-    // library's merged resolve re-derives what it needs, so no n*M*8-byte region here
-#ifdef MIVQ_CS_TIMESTAMPS
-    void* pinfo = ws + off;
-#else
-    void* pinfo = nullptr;
-#endif
 
     const bool aligned = (reinterpret_cast<uintptr_t>(x) % 16 == 0) && (d % 4 == 0) && (L.dsub % 4 == 0);
     const bool exact_only = (flags_in & MIVQ_PQ_FORCE_EXACT) != 0;
@@ -858,7 +848,7 @@ extern "C" int mivq_pq_encode(const float* x, int64_t n, int32_t d, int32_t M, i
             const hipError_t e = launch_pq_encode_cs(L.ks, x + r0 * d, nc, d, M, L.dsub, centroids, cn, p + L.img,
                                                      reinterpret_cast<const float*>(p + L.hinit), p + L.bnd,
                                                      M <= kPdMaxM ? p + L.pd : nullptr, p + L.bnd2, codesT, items,
-                                                     counts, pinfo, u8 + r0 * M, st);
+                                                     counts, u8 + r0 * M, st);
             if (e != hipSuccess) return set_error(MIVQ_ERR_HIP, "pq_encode_cs: %s", hipGetErrorString(e));
         }
     } else if (mfma_ok) {

@@ -52,47 +52,15 @@ typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 
-#ifndef MIVQ_CS_WAVES
-#define MIVQ_CS_WAVES 12
-#endif
-#ifndef MIVQ_CS_ASPLIT
-#define MIVQ_CS_ASPLIT 1
-#endif
-#ifndef MIVQ_CS_KH_CONTIG  // K halves as contiguous row halves (lane half h reads tile half h)
-#define MIVQ_CS_KH_CONTIG 1
-#endif
-#ifndef MIVQ_GC_DS  // wide-subspace resolve: rows in registers, centroid rows loaded whole
-#define MIVQ_GC_DS 1
-#endif
-#ifndef MIVQ_GC_WHOLE_ROW
-#define MIVQ_GC_WHOLE_ROW 0
-#endif
-#ifndef MIVQ_GC_LIST  // wide-subspace resolve: full-batch candidates chained one per lane
-#define MIVQ_GC_LIST 1
-#endif
-#ifndef MIVQ_GC_LIST_NC  // pieces of a centroid row in the list chains (dsub > 128)
-#define MIVQ_GC_LIST_NC 4
-#endif
-constexpr int kWaves = MIVQ_CS_WAVES;  // 768 threads, 3 waves per SIMD (profiling builds may override)
+constexpr int kWaves = 12;  // 768 threads, 3 waves per SIMD
+constexpr int kGcListNc = 4;  // wide-subspace resolve: pieces of a centroid row in the list chains (dsub > 128)
 
 // Wide subspaces (dsub 97..192, KS 7..12): the f16 image alone takes up to 96 KiB of LDS, so
 // the filter runs 4 waves (one per SIMD, up to 512 registers) with two blocks in flight each.
 constexpr int kWideWaves = 4;
 constexpr int cs_waves(int KS) { return KS <= 6 ? kWaves : kWideWaves; }
 constexpr int kRsrcWord3 = 0x00020000;  // gfx9 buffer resource: 32-bit data format
-#ifndef MIVQ_CS_XAUX
-#define MIVQ_CS_XAUX 2
-#endif
-constexpr int kXAux = MIVQ_CS_XAUX;  // x stream cache policy: nt (read once)
-#ifndef MIVQ_CS_PRIO  // profiling: s_setprio 1 around each centroid block's MFMAs
-#define MIVQ_CS_PRIO 0
-#endif
-#ifndef MIVQ_CS_NOPIPE  // 1: one accumulator everywhere (no MFMAs of block cb + 1 during the ranking of cb)
-#define MIVQ_CS_NOPIPE 0
-#endif
-#ifndef MIVQ_CS_PF  // profiling: dword loads that pull the wave's block after next into L2 (line bytes)
-#define MIVQ_CS_PF 0
-#endif
+constexpr int kXAux = 2;  // x stream cache policy: nt (read once; round 4 measured the others)
 
 // Keeps the three largest of a stream of packed scores.  Inline asm because the compiler
 // quiets every packed value (v_max_f32 v, v, v) before fmaxf / fmed3 in IEEE mode: the
@@ -170,20 +138,9 @@ __device__ __forceinline__ float dot2_self(uint32_t u, float acc) {
 
 __device__ __forceinline__ uint32_t lds_addr(const void* p) { return (uint32_t)(uintptr_t)p; }
 
-#ifndef MIVQ_CS_PERMLANE
-#define MIVQ_CS_PERMLANE 0
-#endif
-// Lanes 0..31 receive lane l + 32's value (lanes 32..63: their own value back).  The filter's
-// lane pair (l, l + 32) holds one row; only the h = 0 lanes use the merged result, so a
-// v_permlane32_swap (VALU, no LDS round trip) replaces ds_bpermute's __shfl_xor(v, 32).
-__device__ __forceinline__ float upper_half(float v) {
-#if MIVQ_CS_PERMLANE
-    const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
-    return __uint_as_float(r[1]);
-#else
-    return __shfl_xor(v, 32);
-#endif
-}
+// Lanes 0..31 receive lane l + 32's value.  The filter's lane pair (l, l + 32) holds one row;
+// only the h = 0 lanes use the merged result.  (v_permlane32_swap measured the same.)
+__device__ __forceinline__ float upper_half(float v) { return __shfl_xor(v, 32); }
 
 // 8 x reads (stride XS bytes) and the 4 reads of two centroid-pair rows (CS bytes apart),
 // all issued back to back, then one lgkmcnt(0).
@@ -216,16 +173,7 @@ __device__ __forceinline__ void lds_burst(uint32_t xa, uint32_t ca, f32x4 (&xq)[
 // the grid allows, each XCD gets all M subspaces of a chunk in consecutive slots, so the M
 // workgroups reading one row range run side by side on one XCD and sweep the same DRAM pages
 // together.  Both kernels of the encode use the same mapping (the lists are per workgroup).
-#ifndef MIVQ_CS_XCDM  // profiling: XCD x takes subspaces m = x (mod 8), every chunk (M % 8 == 0)
-#define MIVQ_CS_XCDM 0
-#endif
 __device__ __forceinline__ void wg_coords_of(unsigned b, unsigned g, int M, int& m, int64_t& chunk) {
-    if (MIVQ_CS_XCDM && M % 8 == 0 && g % (8u * (unsigned)M) == 0) {
-        const unsigned j = b >> 3, per = (unsigned)M / 8u;
-        m = (int)((b & 7u) + 8u * (j % per));
-        chunk = (int64_t)(j / per);
-        return;
-    }
     if (g % (8u * (unsigned)M) == 0) {
         const unsigned j = b >> 3;
         m = (int)(j % (unsigned)M);
@@ -247,20 +195,6 @@ constexpr int max_loads() {
 }
 
 
-// V: profiling variants (tools/cs_variants.hip), 0 in the library.  Bits drop work and
-// produce wrong codes: 1 the resolve kernel, 2 its full scans, 4 its pair checks, 8 its x
-// reads, 16 the whole filter, 32 all but the first 32 centroids of the filter, 64 the x
-// loads after a wave's second vb (compute alone), 128 reads the same bytes as if x were
-// stored subspace-major (contiguous per workgroup: a memory-pattern probe), 256 settles full
-// items with the pair kernel's 256-wide exact scans instead of pq_resolve_full_kernel, 512
-// makes the LDS-codebook full-item kernel count (into `counts`) its rows, whole-row scans and
-// candidates; with 512: 1024 skips its exact chains, 2048 runs one filter block, 4096 gathers
-// row 0 only.  Exact alternatives (same codes): 16384 the lane-wide top-3 filter instead of
-// the grouped top-2, 32768 no pair window in the pair kernel, 65536 the LDS-codebook
-// full-item kernel (pq_resolve_full_kernel) instead of pq_resolve_full2_kernel.  131072 (wrong
-// codes): every centroid block reuses block 0's A fragments (an LDS-read probe).  262144 (codes
-// exact): the pair kernel stores (pairs settled by the pair window, pairs gathered) per
-// workgroup into `counts`.
 // DS > 0: the kernel for sub-rows of exactly DS floats (the addresses and load counts fold
 // to constants); DS = 0 reads dsub at run time.
 // KH = 2 (wide subspaces with dsub == 16 KS, KS even): the wave's tile holds half of the
@@ -269,13 +203,13 @@ constexpr int max_loads() {
 // Image K-step g gives lane half h the dims 8 KS h + 8 g + [0, 8), so tile half hh holds the
 // dims hh 8 KT + [0, 8 KT) and 8 KS + hh 8 KT + [0, 8 KT) (KT = KS / 2): two 32 KT-byte
 // segments of each row.
-template <int KS, int LAYOUT, int V = 0, int DS = 0, int NW = kWaves, int KH = 1>
+template <int KS, int LAYOUT, int DS = 0, int NW = kWaves, int KH = 1>
 __global__ __launch_bounds__(NW * 64) void pq_encode_cs_kernel(
     const float* __restrict__ x, int64_t n, int d, int M, int dsub_in, int64_t rows_per_wg,
     const float* __restrict__ C, const float* __restrict__ cn, const half8* __restrict__ img,
     const float* __restrict__ hinit, const float4* __restrict__ bnd, uint8_t* __restrict__ codesT,
-    uint2* __restrict__ items, int2* __restrict__ counts, float2* __restrict__ pinfo,
-    const float2* __restrict__ pdw, const float4* __restrict__ bnd2) {
+    uint2* __restrict__ items, int2* __restrict__ counts, const float2* __restrict__ pdw,
+    const float4* __restrict__ bnd2) {
     static_assert(KH == 1 || (KH == 2 && KS % 2 == 0), "K halves");
     constexpr int FR = 8 * KS * 64;
     constexpr int KT = KS / KH;          // K-steps per tile fill
@@ -285,10 +219,7 @@ __global__ __launch_bounds__(NW * 64) void pq_encode_cs_kernel(
     half8* cimg = reinterpret_cast<half8*>(smem);
     unsigned char* stg_all = smem + FR * 16;
     constexpr int NT = NW * 64;
-#ifndef MIVQ_CS_KDEP  // x blocks in flight per wave for the full-occupancy filters (profiling builds: 2)
-#define MIVQ_CS_KDEP 1
-#endif
-    constexpr int kDep = (NW >= kWaves || KH > 1) ? MIVQ_CS_KDEP : 2;  // x blocks in flight per wave
+    constexpr int kDep = (NW >= kWaves || KH > 1) ? 1 : 2;  // x blocks in flight per wave
     float* hb = reinterpret_cast<float*>(stg_all + NW * 32 * PITCH);
     float* cnl = hb + 256;
     int* ctr = reinterpret_cast<int*>(cnl + 256);  // [0] pairs, [1] full, [2] resolve batches
@@ -305,9 +236,6 @@ __global__ __launch_bounds__(NW * 64) void pq_encode_cs_kernel(
     const int64_t r1 = min(n, r0 + rows_per_wg);
     if (r0 >= r1) return;
     const int nrows = (int)(r1 - r0);
-#ifdef MIVQ_CS_TIMESTAMPS  // probe (tools/dbg/wg_times.py): start / end of every workgroup
-    const uint64_t t_start = wall_clock64();
-#endif
 
     {  // stage the subspace's fp16 codebook image, norms; zero the tiles (pad columns stay 0)
         const half8* src = img + (int64_t)m * FR;
@@ -330,7 +258,7 @@ __global__ __launch_bounds__(NW * 64) void pq_encode_cs_kernel(
     // so P per-lane offsets suffice.
     const int dsub_h = dsub / KH;            // floats per tile fill (KH = 2: dsub == 16 KS)
     const int q = dsub_h >> 2;               // 16-B chunks per row and tile fill
-    const int XS = (V & 128) ? dsub : d;     // row stride of the loads (V&128: subspace-major probe)
+    const int XS = d;                        // row stride of the loads
     constexpr int PER = LAYOUT == 0 ? 1 : LAYOUT;
     const int rpi = LAYOUT == 0 ? min(32, 64 / q) : 64 * PER / q;  // rows per instruction / period
     const int ni = LAYOUT == 0 ? (32 + rpi - 1) / rpi : q / 2;
@@ -341,7 +269,7 @@ __global__ __launch_bounds__(NW * 64) void pq_encode_cs_kernel(
         const int c = LAYOUT == 0 ? l : 64 * sidx + l;
         prow[sidx] = c / q;
         const int col = c - prow[sidx] * q;
-        const int gcol = (KH == 1 || MIVQ_CS_KH_CONTIG) ? 4 * col : 4 * col + (col >= 2 * KT ? 8 * KS - 8 * KT : 0);
+        const int gcol = 4 * col;
         voff[sidx] = (prow[sidx] * XS + gcol) * 4;
         toff[sidx] = prow[sidx] * PITCH + 8 * col;
     }
@@ -350,7 +278,7 @@ __global__ __launch_bounds__(NW * 64) void pq_encode_cs_kernel(
     // rows past the range read as zeros without a branch; idle lanes of LAYOUT 0 get a
     // voffset >= 2^31, past any range.
     const __amdgpu_buffer_rsrc_t xr_rsrc = __builtin_amdgcn_make_buffer_rsrc(
-        (void*)(x + ((V & 128) ? ((int64_t)m * n + r0) * dsub : r0 * d + (int64_t)m * dsub)), 0,
+        (void*)(x + r0 * d + (int64_t)m * dsub), 0,
         (int)(((int64_t)(nrows - 1) * XS + dsub) * 4), kRsrcWord3);
 #pragma unroll
     for (int sidx = 0; sidx < PER; ++sidx)
@@ -374,7 +302,7 @@ __global__ __launch_bounds__(NW * 64) void pq_encode_cs_kernel(
             if (i < ni) {  // uniform
                 // the block's uniform offset goes in soffset (SALU; gfx950 range-checks
                 // voffset + soffset, tools/probes/soffset_range.hip), the lane's in voffset
-                const int so = (vb * 32 + ibase(i)) * XS * 4 + hh * ((MIVQ_CS_KH_CONTIG ? 16 : 8) * KT * 4);
+                const int so = (vb * 32 + ibase(i)) * XS * 4 + hh * (16 * KT * 4);
                 const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(xr_rsrc, voff[i % PER], so, kXAux);
                 dst[i] = make_float4(__uint_as_float(v[0]), __uint_as_float(v[1]), __uint_as_float(v[2]),
                                      __uint_as_float(v[3]));
@@ -393,66 +321,28 @@ __global__ __launch_bounds__(NW * 64) void pq_encode_cs_kernel(
     // tail): as a loop-carried load result, the compiler copied it at the loop latch, i.e. waited
     // vmcnt(0) -- for the next x block's refill too -- at the end of every step.  M > 64 (no
     // per-pair spreads prepared): every pair goes to the list.
-    constexpr bool kLegacyPairs = (V & (1 << 20)) != 0;  // round-1 pair kernel (profiling)
     const bool pd_on = pdw != nullptr;
     const float2* pdsrc = pd_on ? pdw : reinterpret_cast<const float2*>(bnd2);
     const float4 b2 = pd_on ? bnd2[m] : make_float4(0.f, 0.f, 0.f, 0.f);
     // The pending pair's spreads: every lane loads (a pair-less lane, or M > 64, reads a valid
     // 8 B that is never used), so no branch surrounds the load.
-#ifndef MIVQ_CS_PD_EARLY  // 1: the pending pair's load at the next step's start; 0: at the tail
-#define MIVQ_CS_PD_EARLY 1
-#endif
-#ifndef MIVQ_CS_REFILL_COND  // profiling: round-3 conditional refill
-#define MIVQ_CS_REFILL_COND 0
-#endif
-#ifndef MIVQ_CS_PIN
-#define MIVQ_CS_PIN 1
-#endif
-#ifndef MIVQ_CS_D64_R3  // profiling: dsub 64 (16 waves at 128 VGPRs) on the round-3 loop structure
-#define MIVQ_CS_D64_R3 0
-#endif
     // dsub 64 at 16 waves: the round-4 loop with both accumulators spills (20-140 B per lane,
     // 3 % slower), so that kernel runs it with ONE accumulator (kNoPipe: the next centroid
     // block's MFMAs wait for this block's ranking; the other three waves of the SIMD overlap
-    // them): 122 VGPRs, 6.52 -> 6.47 ms per 6.65M x 1024 call (profiles/r04_s19).  With
-    // MIVQ_CS_D64_R3 it keeps round 3's structure (refill under its branch, the pair load at
-    // the tail, the sigma test per block), as the generic shapes (DS == 0) do: their register
-    // budgets differ per KS.
-    constexpr bool kR3Loop = (DS == 64 && NW == 16 && MIVQ_CS_D64_R3) || DS == 0;
-    constexpr bool kNoPipe = MIVQ_CS_NOPIPE || (DS == 64 && NW == 16 && !MIVQ_CS_D64_R3);
-    constexpr bool kPdEarly = MIVQ_CS_PD_EARLY && !kR3Loop;
-    constexpr bool kRefillCond = MIVQ_CS_REFILL_COND || kR3Loop;
-    constexpr bool kPin = MIVQ_CS_PIN && !kR3Loop;
+    // them): 122 VGPRs, 6.52 -> 6.47 ms per 6.65M x 1024 call (profiles/r04_s19).  The generic
+    // shapes (DS == 0) keep round 3's structure (refill under its branch, the pair load at the
+    // tail, the sigma test per block): their register budgets differ per KS.  (Measured and
+    // dropped, round 4: a fixed count of range-checked stores per step, profiles/r04_s9, r04_s28.)
+    constexpr bool kR3Loop = DS == 0;
+    constexpr bool kNoPipe = DS == 64 && NW == 16;
+    constexpr bool kPdEarly = !kR3Loop;
+    constexpr bool kRefillCond = kR3Loop;
+    constexpr bool kPin = !kR3Loop;
     auto load_pending_pd = [&]() __attribute__((always_inline)) {
-        if constexpr (!kLegacyPairs) {
-            const bool on = pd_on && pend_row >= 0;
-            pend_pd = pdsrc[((int64_t)(pd_on ? m : 0) * 256 + (on ? (pend_k & 0xFF) : 0)) * 256 +
-                            (on ? (pend_k >> 8) : 0)];
-        }
-    };
-#ifndef MIVQ_CS_FIXED_STORES  // every step issues the same number of global stores (see below)
-#define MIVQ_CS_FIXED_STORES 0
-#endif
-    // Fixed store count (round-4 loop): the code / list stores of a step go out as buffer stores
-    // from every lane, non-writers with an out-of-range offset (dropped by the range check), and
-    // no branch skips them.  With a data-dependent number of stores the compiler cannot count
-    // them, so the next block's staging waited vmcnt(0) -- for this tail's stores too.
-    constexpr bool kFixedStores = MIVQ_CS_FIXED_STORES && !kR3Loop && !kLegacyPairs;
-    const __amdgpu_buffer_rsrc_t code_rsrc =
-        __builtin_amdgcn_make_buffer_rsrc((void*)(codesT + (int64_t)m * n + r0), 0, nrows, kRsrcWord3);
-    const __amdgpu_buffer_rsrc_t list_rsrc =
-        __builtin_amdgcn_make_buffer_rsrc((void*)(items + (int64_t)m * n + r0), 0, nrows * 8, kRsrcWord3);
-    constexpr int kOob = (int)0x80000000u;
-    // the pending pair, settled or listed without branches (kFixedStores): returns "to the list"
-    auto settle_pending_fixed = [&]() __attribute__((always_inline)) {
-        const float w12 = 1.0625f * (fmaf(4.8828125e-4f, pend_xs, b2.z) * pend_pd.x + pend_xs * pend_pd.y +
-                                     b2.x * pend_xs + b2.y);
-        const bool settled = pend_row >= 0 && pd_on && pend_gap > w12;
-        __builtin_amdgcn_raw_buffer_store_b8((uint8_t)(pend_k & 0xFF), code_rsrc, settled ? pend_row : kOob, 0, 0);
-        return pend_row >= 0 && !settled;
+        const bool on = pd_on && pend_row >= 0;
+        pend_pd = pdsrc[((int64_t)(pd_on ? m : 0) * 256 + (on ? (pend_k & 0xFF) : 0)) * 256 + (on ? (pend_k >> 8) : 0)];
     };
     auto settle_pending = [&]() __attribute__((always_inline)) {
-        if constexpr (kFixedStores) return settle_pending_fixed();
         if (pend_row < 0) return false;
         if (!pd_on) return true;
         const float w12 = 1.0625f * (fmaf(4.8828125e-4f, pend_xs, b2.z) * pend_pd.x + pend_xs * pend_pd.y +
@@ -465,26 +355,9 @@ __global__ __launch_bounds__(NW * 64) void pq_encode_cs_kernel(
     };
     // Appends this wave's pair items (row prow, candidates pk) and full items (row frow) to the
     // workgroup's lists: pairs from the front, full items from the back.
-    auto append = [&](bool isp, int prow, int pk, float pgap, float pxs, bool isf, int frow)
-                      __attribute__((always_inline)) {
+    auto append = [&](bool isp, int prow, int pk, bool isf, int frow) __attribute__((always_inline)) {
         const uint64_t bp = __ballot(isp);
         const uint64_t bfull = __ballot(isf);
-        if constexpr (kFixedStores) {
-            int basep = 0, basef = 0;
-            if (l == 0) {  // LDS atomics (lgkmcnt): adding 0 is harmless
-                basep = atomicAdd(&ctr[0], __popcll(bp));
-                basef = atomicAdd(&ctr[1], __popcll(bfull));
-            }
-            basep = __shfl(basep, 0);
-            basef = __shfl(basef, 0);
-            const uint64_t below = (1ull << l) - 1ull;
-            const int atp = basep + __popcll(bp & below);
-            const int atf = nrows - 1 - (basef + __popcll(bfull & below));
-            const u32x2 vp = {(uint32_t)prow, (uint32_t)pk}, vf = {(uint32_t)frow, 0u};
-            __builtin_amdgcn_raw_buffer_store_b64(vp, list_rsrc, isp ? atp * 8 : kOob, 0, 0);
-            __builtin_amdgcn_raw_buffer_store_b64(vf, list_rsrc, isf ? atf * 8 : kOob, 0, 0);
-            return;
-        }
         if (bp | bfull) {
             int basep = 0, basef = 0;
             if (l == 0) {
@@ -495,33 +368,8 @@ __global__ __launch_bounds__(NW * 64) void pq_encode_cs_kernel(
             basef = __shfl(basef, 0);
             const uint64_t below = (1ull << l) - 1ull;
             uint2* list = items + (int64_t)m * n + r0;
-            if (isp) {
-                const int at = basep + __popcll(bp & below);
-                list[at] = make_uint2((uint32_t)prow, (uint32_t)pk);
-                // the legacy pair kernel's own window needs the score gap and Xs
-                if (kLegacyPairs && pinfo != nullptr) pinfo[(int64_t)m * n + r0 + at] = make_float2(pgap, pxs);
-            }
+            if (isp) list[basep + __popcll(bp & below)] = make_uint2((uint32_t)prow, (uint32_t)pk);
             if (isf) list[nrows - 1 - (basef + __popcll(bfull & below))] = make_uint2((uint32_t)frow, 0u);
-        }
-    };
-
-    // MIVQ_CS_PF = G (profiling): after the refill, one dword per G-byte line of the block after
-    // that goes out (KH == 1), and its value is consumed a step later, so those lines are
-    // in L2 / MALL when the refill of the next step reads them.
-    constexpr int kPfG = MIVQ_CS_PF > 0 ? MIVQ_CS_PF : 64;
-    constexpr int kNpf = (MIVQ_CS_PF > 0 && KH == 1 && DS > 0) ? (32 * DS * 4 / kPfG + 63) / 64 : 0;
-    uint32_t pfv[kNpf > 0 ? kNpf : 1] = {0u};
-    uint32_t pf_sink = 0u;
-    auto prefetch = [&](int pvb) __attribute__((always_inline)) {
-        if constexpr (kNpf > 0) {
-            constexpr int spr = DS * 4 / kPfG;  // lines per row segment
-#pragma unroll
-            for (int j = 0; j < kNpf; ++j) {
-                pf_sink ^= pfv[j];
-                const int s = 64 * j + l, prw = s / spr;
-                const int off = s < 32 * spr ? prw * XS * 4 + (s - prw * spr) * kPfG : (int)0x80000000u;
-                pfv[j] = __builtin_amdgcn_raw_buffer_load_b32(xr_rsrc, off, pvb * 32 * XS * 4, 0);
-            }
         }
     };
 
@@ -563,7 +411,7 @@ __global__ __launch_bounds__(NW * 64) void pq_encode_cs_kernel(
             stage(decltype(kScaled)::value == 1);
         }
         lds_fence();
-        if constexpr (KH > 1 && MIVQ_CS_KH_CONTIG) {
+        if constexpr (KH > 1) {
             // contiguous halves: tile half hh holds dims [hh dsub/2, (hh+1) dsub/2), which are
             // exactly the dims of lane half h == hh for every image K-step (8 KS h + 8 g + j),
             // so those lanes read all KS fragments from it (exec-masked, no VALU) and the row
@@ -592,13 +440,11 @@ __global__ __launch_bounds__(NW * 64) void pq_encode_cs_kernel(
         // so the next block's loads had only one step's compute to land in.)
         // issued before the refill, so its wait at the tail leaves the refill in flight
         if (kPdEarly && hh == 0) load_pending_pd();
-        if ((!kRefillCond || vb + kDep * kProd < nvb) && !((V & 64) && vb >= kProd))
-            load(vb + kDep * kProd, hh, xr);
+        if (!kRefillCond || vb + kDep * kProd < nvb) load(vb + kDep * kProd, hh, xr);
         // keeps the loads here: the scheduler otherwise sinks them below the MFMAs (shorter
         // register live ranges), leaving them only the step's tail to land in
         if (kPin) __builtin_amdgcn_sched_barrier(0);
         }
-        prefetch(vb + (kDep + 1) * kProd);
         xx += upper_half(xx);  // lanes 0..31: the row norm over both halves
 
         // Candidates: the 16 packed scores of centroid block cb in this lane form a group; each
@@ -611,10 +457,8 @@ __global__ __launch_bounds__(NW * 64) void pq_encode_cs_kernel(
         // R is folded into the third slot (t3 := max(t3, R) after each group): R <= t2 always,
         // so the inserts keep t1, t2 exact and t3 = max(third, R), also across the lane-pair
         // merge.  (A pair inside one group becomes a full item: about 1/16 of the pairs.)
-        // V&16384: the plain lane-wide top-3 (4 ops per score) instead.
         float t1 = -INFINITY, t2 = -INFINITY, t3 = -INFINITY;
-        constexpr bool kGroups = (V & 16384) == 0;
-        constexpr int NCB = (V & 16) ? 0 : (V & 32) ? 1 : 8;
+        constexpr int NCB = 8;
         // MFMAs of centroid block cb+1 go into the other accumulator before the top-3 of cb
         // reads this one, so a wave's matrix and vector work overlap
         // KH = 2: the A fragments in two halves (a scheduling barrier between them), so at most
@@ -627,68 +471,42 @@ __global__ __launch_bounds__(NW * 64) void pq_encode_cs_kernel(
                 acc[4 * qq + 0] = hv.x; acc[4 * qq + 1] = hv.y;
                 acc[4 * qq + 2] = hv.z; acc[4 * qq + 3] = hv.w;
             }
-            constexpr int NP = (KH > 1 && MIVQ_CS_ASPLIT) ? 2 : 1;
-            if (MIVQ_CS_PRIO) __builtin_amdgcn_s_setprio(1);
+            constexpr int NP = KH > 1 ? 2 : 1;
 #pragma unroll
             for (int part = 0; part < NP; ++part) {
                 half8 a[KS / NP];
 #pragma unroll
                 for (int ks = 0; ks < KS / NP; ++ks)
-                    a[ks] = cimg[(((V & 131072) ? 0 : cb) * KS + part * (KS / NP) + ks) * 64 + l];
+                    a[ks] = cimg[(cb * KS + part * (KS / NP) + ks) * 64 + l];
 #pragma unroll
                 for (int ks = 0; ks < KS / NP; ++ks)
                     acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(a[ks], bf[part * (KS / NP) + ks], acc, 0, 0, 0);
                 if (NP > 1 && part == 0) __builtin_amdgcn_sched_barrier(0);
             }
-            if (MIVQ_CS_PRIO) __builtin_amdgcn_s_setprio(0);
             return acc;
         };
-        if constexpr (NCB > 0) {
-
+        {
             floatx16 acc_cur = scores(0);
 #pragma unroll
             for (int cb = 0; cb < NCB; ++cb) {
                 floatx16 acc_next;
                 if (!kNoPipe && cb + 1 < NCB) acc_next = scores(cb + 1);
-                if constexpr (kGroups) {
-#ifndef MIVQ_CS_GROUP  // scores per group (8: half the in-group pairs that become full items)
-#define MIVQ_CS_GROUP 16
-#endif
-                    constexpr int GS = MIVQ_CS_GROUP;
+                {
+                    // a group's first two scores: their max and min (2 ops), then 3 per pair
+                    const float a0 = pack_idx(acc_cur[0], vmask, (uint32_t)(cb * 32));
+                    const float a1 = pack_idx(acc_cur[1], vmask, (uint32_t)(cb * 32 + 1));
+                    float g1, g2;
+                    asm("v_max_f32 %0, %1, %2" : "=v"(g1) : "v"(a0), "v"(a1));
+                    asm("v_min_f32 %0, %1, %2" : "=v"(g2) : "v"(a0), "v"(a1));
 #pragma unroll
-                    for (int g0 = 0; g0 < 16; g0 += GS) {
-                        // a group's first two scores: their max and min (2 ops), then 3 per pair
-                        const float a0 = pack_idx(acc_cur[g0], vmask, (uint32_t)(cb * 32 + (g0 & 3) + 8 * (g0 >> 2)));
-                        const float a1 = pack_idx(acc_cur[g0 + 1], vmask,
-                                                  (uint32_t)(cb * 32 + ((g0 + 1) & 3) + 8 * ((g0 + 1) >> 2)));
-                        float g1, g2;
-                        asm("v_max_f32 %0, %1, %2" : "=v"(g1) : "v"(a0), "v"(a1));
-                        asm("v_min_f32 %0, %1, %2" : "=v"(g2) : "v"(a0), "v"(a1));
-#pragma unroll
-                        for (int i = g0 + 2; i < g0 + GS; i += 2)
-                            top2_insert2(g1, g2,
-                                         pack_idx(acc_cur[i], vmask, (uint32_t)(cb * 32 + (i & 3) + 8 * (i >> 2))),
-                                         pack_idx(acc_cur[i + 1], vmask,
-                                                  (uint32_t)(cb * 32 + ((i + 1) & 3) + 8 * ((i + 1) >> 2))));
-                        merge_group(t1, t2, t3, g1, g2);
-                    }
-                } else {
-#pragma unroll
-                    for (int i = 0; i < 16; ++i)
-                        top3_insert(t1, t2, t3,
-                                    pack_idx(acc_cur[i], vmask, (uint32_t)(cb * 32 + (i & 3) + 8 * (i >> 2))));
+                    for (int i = 2; i < 16; i += 2)
+                        top2_insert2(g1, g2, pack_idx(acc_cur[i], vmask, (uint32_t)(cb * 32 + (i & 3) + 8 * (i >> 2))),
+                                     pack_idx(acc_cur[i + 1], vmask,
+                                              (uint32_t)(cb * 32 + ((i + 1) & 3) + 8 * ((i + 1) >> 2))));
+                    merge_group(t1, t2, t3, g1, g2);
                 }
                 if (cb + 1 < NCB) acc_cur = kNoPipe ? scores(cb + 1) : acc_next;
             }
-        }
-        if constexpr ((V & 16) != 0) {  // keep the loads and conversions alive
-            uint32_t zz = 0;
-#pragma unroll
-            for (int ks = 0; ks < KS; ++ks) {
-                const u32x4 u = __builtin_bit_cast(u32x4, bf[ks]);
-                zz ^= u[0] ^ u[1] ^ u[2] ^ u[3];
-            }
-            t1 = __uint_as_float(zz & 0x3F0000FFu);
         }
         const uint32_t hbit = (uint32_t)h << 2;
         t1 = __uint_as_float(__float_as_uint(t1) | hbit);
@@ -711,34 +529,31 @@ __global__ __launch_bounds__(NW * 64) void pq_encode_cs_kernel(
         const int k2 = (int)(__float_as_uint(t2) & 0xFFu);
         const int rowl = vb * 32 + r;
         const bool mine = (h == 0) && rowl < nrows;
-        if constexpr (kFixedStores)
-            __builtin_amdgcn_raw_buffer_store_b8((uint8_t)k1, code_rsrc, mine && ncand == 1 ? rowl : kOob, 0, 0);
-        else if (mine && ncand == 1)
-            codesT[(int64_t)m * n + r0 + rowl] = (uint8_t)k1;
+        if (mine && ncand == 1) codesT[(int64_t)m * n + r0 + rowl] = (uint8_t)k1;
         const float gap = __fmul_rn(__fsub_rn(t1, t2), 0.99999988f);  // rounded down
-        if (kR3Loop && !kLegacyPairs && pdw != nullptr) {
+        if (kR3Loop && pdw != nullptr) {
             // round-3 tail (dsub 64, generic shapes): settle the previous block's pair, then
             // load this block's pair spreads (a runtime branch: M > 64 appends pairs directly)
             const bool listp = settle_pending();
-            append(listp, pend_row, pend_k, 0.0f, 0.0f, mine && ncand >= 3, rowl);
+            append(listp, pend_row, pend_k, mine && ncand >= 3, rowl);
             const bool np = mine && ncand == 2;
             pend_pd = pdw[((int64_t)m * 256 + (np ? k1 : 0)) * 256 + (np ? k2 : 0)];
             pend_row = np ? rowl : -1;
             pend_k = k1 | (k2 << 8);
             pend_gap = gap;
             pend_xs = Xs;
-        } else if (!kR3Loop && !kLegacyPairs) {
+        } else if (!kR3Loop) {
             // The previous block's pair (its pd load went out before this block's refill): k1
             // is the code when the gap exceeds the pair's own window, else it goes to the list.
             const bool listp = settle_pending();
-            append(listp, pend_row, pend_k, 0.0f, 0.0f, mine && ncand >= 3, rowl);
+            append(listp, pend_row, pend_k, mine && ncand >= 3, rowl);
             pend_row = mine && ncand == 2 ? rowl : -1;
             pend_k = k1 | (k2 << 8);
             pend_gap = gap;
             pend_xs = Xs;
             if (!kPdEarly) load_pending_pd();
         } else {
-            append(mine && ncand == 2, rowl, k1 | (k2 << 8), gap, Xs, mine && ncand >= 3, rowl);
+            append(mine && ncand == 2, rowl, k1 | (k2 << 8), mine && ncand >= 3, rowl);  // M > 64: no pair window
         }
     };
     auto run = [&](auto kScaled) __attribute__((always_inline)) {
@@ -748,14 +563,6 @@ __global__ __launch_bounds__(NW * 64) void pq_encode_cs_kernel(
         for (int hh = 0; hh < KH; ++hh) {
             if (vb < nvb) load(vb, hh, xa[hh]);
             if (kDep == 2 && vb + kProd < nvb) load(vb + kProd, hh, xb[hh]);
-        }
-        if constexpr (kFixedStores) {
-            // the loop's four stores per step, dropped (out of range): the first iteration then
-            // sees the same count of operations after its x loads as every later one
-            __builtin_amdgcn_raw_buffer_store_b8((uint8_t)0, code_rsrc, kOob, 0, 0);
-            __builtin_amdgcn_raw_buffer_store_b8((uint8_t)0, code_rsrc, kOob, 0, 0);
-            __builtin_amdgcn_raw_buffer_store_b64((u32x2){0u, 0u}, list_rsrc, kOob, 0, 0);
-            __builtin_amdgcn_raw_buffer_store_b64((u32x2){0u, 0u}, list_rsrc, kOob, 0, 0);
         }
         for (; vb < nvb; vb += kDep * kProd) {
             step(kScaled, vb, xa);
@@ -772,711 +579,14 @@ __global__ __launch_bounds__(NW * 64) void pq_encode_cs_kernel(
         else
             run(std::integral_constant<int, 1>{});
     }
-    {
-        if (!kLegacyPairs && (!kR3Loop || pdw != nullptr)) {
-            if (kPdEarly) load_pending_pd();
-            const bool listp = settle_pending();
-            append(listp, pend_row, pend_k, 0.0f, 0.0f, false, 0);
-        }
-        if constexpr (kNpf > 0) {  // keeps the prefetch loads alive (never true: n >= 0)
-#pragma unroll
-            for (int j = 0; j < kNpf; ++j) pf_sink ^= pfv[j];
-            if (n < 0 && pf_sink == 0x9E3779B9u) codesT[0] = 0;
-        }
+    if (!kR3Loop || pdw != nullptr) {  // the last block's pending pair
+        if (kPdEarly) load_pending_pd();
+        const bool listp = settle_pending();
+        append(listp, pend_row, pend_k, false, 0);
     }
     }  // producers
     __syncthreads();
     if (tid == 0) counts[blockIdx.x] = make_int2(ctr[0], ctr[1]);
-#ifdef MIVQ_CS_TIMESTAMPS  // (into the pair-info region, unused on this path)
-    if (tid == 0) {
-        reinterpret_cast<unsigned long long*>(pinfo)[2 * blockIdx.x] = t_start;
-        reinterpret_cast<unsigned long long*>(pinfo)[2 * blockIdx.x + 1] = wall_clock64();
-    }
-#endif
-}
-
-// Resolve: settles the lists of one encode workgroup (same blockIdx -> (chunk, m) mapping).
-// LDS: the exact fp32 C_m with centroid pairs (kp, kp+128) interleaved and zero-padded to
-// 16*KS dimensions (the chains run over the padding without guards: fmaf(0, 0, acc) leaves
-// acc's value unchanged), the norms, and a 16-row x staging tile per wave.  Each wave takes
-// batches of 64 items of one kind; their x sub-rows are gathered 16 at a time with loads
-// whose wave-instruction covers 2-3 whole sub-rows.  A pair item runs on one lane (the
-// canonical fmaf chains of its two candidates); a full item is scanned by the whole wave,
-// four centroids per lane as two v_pk_fma_f32 chains, then an (s, k) minimum across lanes.
-constexpr int kRWaves = 8;
-
-template <int KS>
-constexpr int resolve_smem_bytes() {
-    return 128 * (2 * 16 * KS + 4) * 4 + 256 * 4 + kRWaves * 16 * (16 * KS + 4) * 4 + 16 + kRWaves * 64 * 8;
-}
-
-template <int KS, int V = 0>
-__global__ __launch_bounds__(kRWaves * 64) void pq_resolve_cs_kernel(
-    const float* __restrict__ x, int64_t n, int d, int M, int dsub, int64_t rows_per_wg,
-    const float* __restrict__ C, const float* __restrict__ cn, uint8_t* __restrict__ codesT,
-    const uint2* __restrict__ items, const int2* __restrict__ counts, int with_full, const float2* __restrict__ pd,
-    const float4* __restrict__ bnd2, const float2* __restrict__ pinfo) {
-    constexpr int DP = 16 * KS;
-    constexpr int PP = 2 * DP + 4;  // floats per centroid-pair row
-    constexpr int SP = DP + 4;      // floats per staged x row
-    constexpr int NX = DP / 4;      // float4 per padded sub-row
-    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-    float* cp = reinterpret_cast<float*>(smem);
-    float* cnl = cp + 128 * PP;
-    float* stg_all = cnl + 256;
-    int* ctr = reinterpret_cast<int*>(stg_all + kRWaves * 16 * SP);
-    uint2* comp_all = reinterpret_cast<uint2*>(ctr + 4);  // per wave: 64 compacted pair items
-
-    const int tid = threadIdx.x;
-    const int w = tid >> 6, l = tid & 63;
-    int m;
-    int64_t chunk;
-    wg_coords(M, m, chunk);
-    const int64_t r0 = chunk * rows_per_wg;
-    const int64_t r1 = min(n, r0 + rows_per_wg);
-    if (r0 >= r1) return;
-    const int nrows = (int)(r1 - r0);
-    const int2 cnt = counts[blockIdx.x];
-    const int np = cnt.x, nf = with_full ? cnt.y : 0;
-    if (np + nf == 0) return;
-
-    {  // pairs (kp, kp + 128) interleaved; 16-B loads, 4 chunk pairs in flight per thread
-        const float* Cm = C + (int64_t)m * 256 * dsub;
-        const int q4 = DP >> 2, tot = 128 * q4;
-        for (int e0 = tid; e0 < tot; e0 += 4 * kRWaves * 64) {
-            f32x4 va[4], vb[4];
-#pragma unroll
-            for (int u = 0; u < 4; ++u) {
-                const int e = e0 + u * kRWaves * 64;
-                const int kp = e / q4, j = e - kp * q4;
-                const bool in = e < tot && 4 * j < dsub;
-                va[u] = in ? *reinterpret_cast<const f32x4*>(Cm + (int64_t)kp * dsub + 4 * j) : (f32x4){0.f, 0.f, 0.f, 0.f};
-                vb[u] = in ? *reinterpret_cast<const f32x4*>(Cm + (int64_t)(kp + 128) * dsub + 4 * j)
-                           : (f32x4){0.f, 0.f, 0.f, 0.f};
-            }
-#pragma unroll
-            for (int u = 0; u < 4; ++u) {
-                const int e = e0 + u * kRWaves * 64;
-                const int kp = e / q4, j = e - kp * q4;
-                if (e < tot) {
-                    f32x4* dst = reinterpret_cast<f32x4*>(cp + kp * PP + 8 * j);
-                    dst[0] = (f32x4){va[u].x, vb[u].x, va[u].y, vb[u].y};
-                    dst[1] = (f32x4){va[u].z, vb[u].z, va[u].w, vb[u].w};
-                }
-            }
-        }
-        if (tid < 256) cnl[tid] = cn[(int64_t)m * 256 + tid];
-        if (tid == 0) ctr[0] = 0;
-        if ((V & 262144) && tid == 0) ctr[1] = ctr[2] = 0;
-    }
-    __syncthreads();
-
-    const int q = dsub >> 2;
-    const int nld = (16 * q + 63) >> 6;  // load instructions per 16 staged rows
-    // batches: the heavy full items first (16 per batch, for balance), then pairs (64)
-    const int nbf = (nf + 15) >> 4, nbp = (np + 63) >> 6;
-    const uint2* list = items + (int64_t)m * n + r0;
-    const float* xsub = x + r0 * d + (int64_t)m * dsub;
-    float* stg = stg_all + w * 16 * SP;
-    // Stage sub-rows of items [first + 16*pc, +16) (row offsets in rowl of lanes 16*pc..) into
-    // the tile; loads of a piece are issued one piece ahead, each wave-instruction covering
-    // 2-3 whole sub-rows.
-    auto issue = [&](int pc, int cntb, int rowl, f32x4 (&dst)[KS]) __attribute__((always_inline)) {
-#pragma unroll
-        for (int j = 0; j < KS; ++j) {
-            const int c = j * 64 + l;
-            const int ir = c / q, ch = c - ir * q;
-            const int src = __shfl(rowl, min(pc * 16 + ir, 63));
-            // lanes without a chunk load a harmless in-range address (row 0) instead of branching
-            const bool ok = j < nld && ir < 16 && pc * 16 + ir < cntb;
-            dst[j] = *reinterpret_cast<const f32x4*>(xsub + (ok ? (int64_t)src * d + 4 * ch : 0));
-        }
-    };
-    auto stage = [&](int pc, int cntb, const f32x4 (&src)[KS]) __attribute__((always_inline)) {
-#pragma unroll
-        for (int j = 0; j < KS; ++j) {
-            const int c = j * 64 + l;
-            const int ir = c / q, ch = c - ir * q;
-            if (j < nld && ir < 16 && pc * 16 + ir < cntb)
-                *reinterpret_cast<f32x4*>(stg + ir * SP + 4 * ch) = src[j];
-        }
-        lds_fence();
-    };
-
-    for (;;) {
-        int b = 0;
-        if (l == 0) b = atomicAdd(&ctr[0], 1);
-        b = __shfl(b, 0);
-        if (b >= nbp + nbf) break;
-        f32x4 ga[KS], gb[KS];
-        if (b < nbf) {
-            // ---- 16 full items: the wave scans G staged rows at a time, lane l taking the
-            // centroid pairs (l, l+128) and (l+64, l+192) of each: 2G independent
-            // v_pk_fma_f32 chains, and each centroid read serves G rows
-            const int first = b * 16;
-            const int cntb = min(16, nf - first);
-            int rowl = 0;
-            if (l < cntb) rowl = (int)list[nrows - 1 - (first + l)].x;
-            issue(0, cntb, rowl, ga);
-            stage(0, cntb, ga);
-            if constexpr ((V & 10) != 0) { lds_fence(); continue; }
-            constexpr int G = 8;
-            const float* ca = cp + l * PP;
-            for (int g0 = 0; g0 < cntb; g0 += G) {
-                float2v a[G], bb[G];
-#pragma unroll
-                for (int g = 0; g < G; ++g) a[g] = bb[g] = (float2v){0.0f, 0.0f};
-                const float* xg = stg + g0 * SP;  // rows past cntb hold stale data: unused
-                const uint32_t xa0 = lds_addr(xg), ca0 = lds_addr(ca);
-#pragma unroll 1
-                for (int i = 0; i < q; ++i) {
-                    // the G x vectors and 4 centroid-pair vectors of step i in one burst, one wait
-                    // (left to itself the compiler issues and waits for the x reads one by one)
-                    f32x4 xq[G], p0, p1, q0, q1;
-                    lds_burst<G, SP * 4, 64 * PP * 4>(xa0 + 16 * i, ca0 + 32 * i, xq, p0, p1, q0, q1);
-#pragma unroll
-                    for (int g = 0; g < G; ++g) {
-                        a[g] = __builtin_elementwise_fma((float2v){xq[g].x, xq[g].x}, (float2v){p0.x, p0.y}, a[g]);
-                        bb[g] = __builtin_elementwise_fma((float2v){xq[g].x, xq[g].x}, (float2v){q0.x, q0.y}, bb[g]);
-                        a[g] = __builtin_elementwise_fma((float2v){xq[g].y, xq[g].y}, (float2v){p0.z, p0.w}, a[g]);
-                        bb[g] = __builtin_elementwise_fma((float2v){xq[g].y, xq[g].y}, (float2v){q0.z, q0.w}, bb[g]);
-                        a[g] = __builtin_elementwise_fma((float2v){xq[g].z, xq[g].z}, (float2v){p1.x, p1.y}, a[g]);
-                        bb[g] = __builtin_elementwise_fma((float2v){xq[g].z, xq[g].z}, (float2v){q1.x, q1.y}, bb[g]);
-                        a[g] = __builtin_elementwise_fma((float2v){xq[g].w, xq[g].w}, (float2v){p1.z, p1.w}, a[g]);
-                        bb[g] = __builtin_elementwise_fma((float2v){xq[g].w, xq[g].w}, (float2v){q1.z, q1.w}, bb[g]);
-                    }
-                }
-                // per row: this lane's 4 centroids in increasing k, then the (s, k) minimum
-                // across lanes (NaN never wins; all-NaN/inf rows give 0)
-                float bs[G];
-                int bk[G];
-#pragma unroll
-                for (int g = 0; g < G; ++g) {
-                    bs[g] = INFINITY;
-                    bk[g] = l;
-                    const float s0 = __builtin_fmaf(-2.0f, a[g].x, cnl[l]);
-                    const float s1 = __builtin_fmaf(-2.0f, bb[g].x, cnl[l + 64]);
-                    const float s2 = __builtin_fmaf(-2.0f, a[g].y, cnl[l + 128]);
-                    const float s3 = __builtin_fmaf(-2.0f, bb[g].y, cnl[l + 192]);
-                    if (s0 < bs[g]) { bs[g] = s0; bk[g] = l; }
-                    if (s1 < bs[g]) { bs[g] = s1; bk[g] = l + 64; }
-                    if (s2 < bs[g]) { bs[g] = s2; bk[g] = l + 128; }
-                    if (s3 < bs[g]) { bs[g] = s3; bk[g] = l + 192; }
-                }
-#pragma unroll
-                for (int o = 32; o > 0; o >>= 1) {
-#pragma unroll
-                    for (int g = 0; g < G; ++g) {
-                        const float os = __shfl_xor(bs[g], o);
-                        const int ok = __shfl_xor(bk[g], o);
-                        if (os < bs[g] || (os == bs[g] && ok < bk[g])) { bs[g] = os; bk[g] = ok; }
-                    }
-                }
-#pragma unroll
-                for (int g = 0; g < G; ++g) {
-                    const int rw = __shfl(rowl, min(g0 + g, 63));
-                    if (l == 0 && g0 + g < cntb)
-                        codesT[(int64_t)m * n + r0 + rw] = (uint8_t)((bs[g] < INFINITY) ? bk[g] : 0);
-                }
-            }
-            lds_fence();
-        } else {
-            // ---- 64 pairs, one per lane: the canonical chains of its two candidates
-            const int first = (b - nbf) * 64;
-            const int cnt0 = min(64, np - first);
-            uint2 it = make_uint2(0u, 0u);
-            bool keep = l < cnt0;
-            if (keep) it = list[first + l];
-            if (pd != nullptr && keep) {
-                // The pair's own window: the f16 rounding of the score difference of k1 and k2
-                // is bounded with ||c~_k1 - c~_k2|| and ||dc_k1 - dc_k2|| instead of the
-                // subspace maxima (the other terms as in the filter window).  If t1 - t2 exceeds
-                // it, k2 cannot be the canonical winner: k1 is the code, no chains needed.
-                const float2 gi = pinfo[(int64_t)m * n + r0 + first + l];
-                const int q1 = (int)(it.y & 0xFFu), q2 = (int)((it.y >> 8) & 0xFFu);
-                const float2 dd = pd[((int64_t)m * 256 + q1) * 256 + q2];
-                const float4 b2 = bnd2[m];
-                const float w12 = 1.0625f * (fmaf(4.8828125e-4f, gi.y, b2.z) * dd.x + gi.y * dd.y +
-                                             b2.x * gi.y + b2.y);
-                if (gi.x > w12) {
-                    codesT[(int64_t)m * n + r0 + it.x] = (uint8_t)q1;
-                    keep = false;
-                }
-            }
-            // compact the remaining items into lanes 0 .. cntb-1
-            const uint64_t km = __ballot(keep);
-            const int cntb = __popcll(km);
-            if ((V & 262144) && l == 0) { atomicAdd(&ctr[1], cnt0 - cntb); atomicAdd(&ctr[2], cntb); }
-            uint2* comp = comp_all + w * 64;
-            if (keep) comp[__popcll(km & ((1ull << l) - 1ull))] = it;
-            lds_fence();
-            const bool live = l < cntb;
-            it = live ? comp[l] : make_uint2(0u, 0u);
-            lds_fence();
-            if (cntb == 0) continue;
-            const int rowl = (int)it.x;
-            float4 xv[NX];
-#pragma unroll
-            for (int i = 0; i < NX; ++i) xv[i] = make_float4(0.f, 0.f, 0.f, 0.f);
-            // the lanes of piece pc copy their staged row; pieces alternate between two
-            // register buffers so that the next piece's loads are always in flight
-            auto take = [&](int pc) __attribute__((always_inline)) {
-                if ((l >> 4) == pc && live) {
-                    const float* xr = stg + (l & 15) * SP;
-#pragma unroll
-                    for (int i = 0; i < NX; ++i)
-                        if (4 * i < dsub) xv[i] = *reinterpret_cast<const float4*>(xr + 4 * i);
-                }
-                lds_fence();
-            };
-            issue(0, cntb, rowl, ga);
-            if (cntb > 16) issue(1, cntb, rowl, gb);
-            stage(0, cntb, ga);
-            take(0);
-            if (cntb > 32) issue(2, cntb, rowl, ga);
-            if (cntb > 16) { stage(1, cntb, gb); take(1); }
-            if (cntb > 48) issue(3, cntb, rowl, gb);
-            if (cntb > 32) { stage(2, cntb, ga); take(2); }
-            if (cntb > 48) { stage(3, cntb, gb); take(3); }
-            if (!live) continue;
-            if constexpr ((V & 12) != 0) continue;
-            const int k1 = (int)(it.y & 0xFFu), k2 = (int)((it.y >> 8) & 0xFFu);
-            const float* c1 = cp + (k1 & 127) * PP + (k1 >> 7);
-            const float* c2 = cp + (k2 & 127) * PP + (k2 >> 7);
-            float d1 = 0.0f, d2 = 0.0f;
-#pragma unroll
-            for (int i = 0; i < NX; ++i) {
-                const int t = 4 * i;
-                d1 = __builtin_fmaf(xv[i].x, c1[2 * t + 0], d1);
-                d2 = __builtin_fmaf(xv[i].x, c2[2 * t + 0], d2);
-                d1 = __builtin_fmaf(xv[i].y, c1[2 * t + 2], d1);
-                d2 = __builtin_fmaf(xv[i].y, c2[2 * t + 2], d2);
-                d1 = __builtin_fmaf(xv[i].z, c1[2 * t + 4], d1);
-                d2 = __builtin_fmaf(xv[i].z, c2[2 * t + 4], d2);
-                d1 = __builtin_fmaf(xv[i].w, c1[2 * t + 6], d1);
-                d2 = __builtin_fmaf(xv[i].w, c2[2 * t + 6], d2);
-            }
-            const float s1 = __builtin_fmaf(-2.0f, d1, cnl[k1]);
-            const float s2 = __builtin_fmaf(-2.0f, d2, cnl[k2]);
-            codesT[(int64_t)m * n + r0 + rowl] = (uint8_t)((s2 < s1 || (s2 == s1 && k2 < k1)) ? k2 : k1);
-        }
-    }
-    if constexpr ((V & 262144) != 0) {  // instrumentation: pairs settled by the pair window / gathered
-        __syncthreads();
-        if (tid == 0) const_cast<int2*>(counts)[blockIdx.x] = make_int2(ctr[1], ctr[2]);
-    }
-}
-
-// Full items (three or more filter candidates inside the window): the filter is re-run for
-// 32 gathered rows at a time — the same f16 operands, accumulator init and window as the
-// encode kernel, but on the unpacked scores — and only the centroids whose score is inside
-// the window get the canonical fp32 chains.  Every minimiser of the canonical score lies
-// inside the window, so the smallest-(s, k) candidate is the canonical code.  Rows the
-// bound cannot vouch for (non-finite, out of range) and rows with more than kFCap
-// candidates are scanned over all 256 centroids.  LDS holds the fp32 codebook (the chains
-// read it; the f16 MFMA operands are converted from it on the fly: f16(tau c), tau = 4 sigma,
-// exactly the prepared image) and, per wave, the 32 fp32 rows and their candidate lists.
-constexpr int kFWaves = 4;
-constexpr int kFCap = 16;
-
-template <int KS>
-constexpr int full_smem_bytes() {
-    return 256 * (16 * KS + 4) * 4 + 256 * 4 + kFWaves * (32 * (16 * KS + 4) * 4 + 32 * kFCap * 4 + 32 * 4);
-}
-
-template <int KS, int V = 0>
-__global__ __launch_bounds__(kFWaves * 64) void pq_resolve_full_kernel(
-    const float* __restrict__ x, int64_t n, int d, int M, int dsub, int64_t rows_per_wg,
-    const float* __restrict__ C, const float* __restrict__ cn, const float* __restrict__ hinit,
-    const float4* __restrict__ bnd, uint8_t* __restrict__ codesT, const uint2* __restrict__ items,
-    const int2* __restrict__ counts) {
-    constexpr int DP = 16 * KS;   // padded dsub
-    constexpr int CP = DP + 4;    // floats per staged centroid row (pad: rows 4 banks apart)
-    constexpr int XP = DP + 4;    // floats per staged x row
-    constexpr int NL = 2 * KS;    // 16-B loads per lane per batch (32 rows of <= DP floats)
-    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-    float* cl = reinterpret_cast<float*>(smem);
-    float* hb = cl + 256 * CP;
-    const int tid = threadIdx.x;
-    const int w = __builtin_amdgcn_readfirstlane(tid >> 6), l = tid & 63;
-    const int r = l & 31, h = l >> 5;
-    float* xf = reinterpret_cast<float*>(reinterpret_cast<unsigned char*>(hb + 256) +
-                                         w * (32 * XP * 4 + 32 * kFCap * 4 + 32 * 4));
-    int* cand = reinterpret_cast<int*>(xf + 32 * XP);
-    int* ccnt = cand + 32 * kFCap;
-
-    int m;
-    int64_t chunk;
-    wg_coords(M, m, chunk);
-    const int64_t r0 = chunk * rows_per_wg;
-    const int64_t r1 = min(n, r0 + rows_per_wg);
-    if (r0 >= r1) return;
-    const int nrows = (int)(r1 - r0);
-    const int nf = counts[blockIdx.x].y;
-    if (nf == 0) return;
-    const float* Cm = C + (int64_t)m * 256 * dsub;
-    {  // 16-B copies, 8 in flight per thread (dsub % 4 == 0 on this path)
-        const int q4 = dsub >> 2, tot = 256 * q4;
-        for (int e0 = tid; e0 < tot; e0 += 8 * kFWaves * 64) {
-            f32x4 v[8];
-#pragma unroll
-            for (int u = 0; u < 8; ++u) {
-                const int e = e0 + u * kFWaves * 64;
-                v[u] = e < tot ? *reinterpret_cast<const f32x4*>(Cm + 4 * (int64_t)e) : (f32x4){0.f, 0.f, 0.f, 0.f};
-            }
-#pragma unroll
-            for (int u = 0; u < 8; ++u) {
-                const int e = e0 + u * kFWaves * 64;
-                const int k = e / q4, j = e - k * q4;
-                if (e < tot) *reinterpret_cast<f32x4*>(cl + k * CP + 4 * j) = v[u];
-            }
-        }
-        for (int e = tid; e < 256 * (DP - dsub); e += kFWaves * 64) {
-            const int k = e / (DP - dsub);
-            cl[k * CP + dsub + (e - k * (DP - dsub))] = 0.0f;
-        }
-    }
-    hb[tid] = hinit[(int64_t)m * 256 + tid];
-    __syncthreads();
-
-    const float4 bm = bnd[m];
-    const float sig1 = bm.x;
-    const float tau1 = bm.w;  // the image's scale (bnd.w)
-    const float xs_eta = 5.9604645e-8f * sqrtf((float)dsub);
-    const float* cnm = cn + (int64_t)m * 256;
-    const int q = dsub >> 2;
-    const int nld = (32 * q + 63) >> 6;
-    const uint2* list = items + (int64_t)m * n + r0;
-    const float* xsub = x + r0 * d + (int64_t)m * dsub;
-    const int nbat = (nf + 31) >> 5;
-
-    auto frag = [&](const float* src, const float sc) __attribute__((always_inline)) {
-        return cvt8_scaled(*reinterpret_cast<const f32x4*>(src), *reinterpret_cast<const f32x4*>(src + 4), sc);
-    };
-
-    // the A operands of all 8 centroid blocks stay in registers for the whole kernel (one
-    // wave per SIMD: 512 registers per lane)
-    half8 aa[8][KS];
-#pragma unroll
-    for (int cb = 0; cb < 8; ++cb) {
-        const float* crow = cl + (cb * 32 + r) * CP + h * 8 * KS;
-#pragma unroll
-        for (int ks = 0; ks < KS; ++ks) aa[cb][ks] = __builtin_bit_cast(half8, frag(crow + 8 * ks, tau1));
-    }
-
-    for (int b = w; b < nbat; b += kFWaves) {
-        const int first = b * 32;
-        const int cntb = min(32, nf - first);
-        int rowl = 0;
-        if (l < cntb) rowl = (int)list[nrows - 1 - (first + l)].x;
-        // gather the 32 fp32 sub-rows (all loads in flight, then the stores), zero the padding
-        f32x4 v[NL];
-#pragma unroll
-        for (int j = 0; j < NL; ++j) {
-            const int c = j * 64 + l;
-            const int row = c / q, col = c - row * q;
-            const int src = __shfl(rowl, min(row, 31));
-            const bool ok = j < nld && row < cntb && !(V & 4096);
-            v[j] = *reinterpret_cast<const f32x4*>(xsub + (ok ? (int64_t)src * d + 4 * col : 0));
-        }
-#pragma unroll
-        for (int j = 0; j < NL; ++j) {
-            const int c = j * 64 + l;
-            const int row = c / q, col = c - row * q;
-            if (j < nld && row < 32) *reinterpret_cast<f32x4*>(xf + row * XP + 4 * col) = v[j];
-        }
-        for (int e = l; e < 32 * (DP - dsub); e += 64) {
-            const int row = e / (DP - dsub);
-            xf[row * XP + dsub + (e - row * (DP - dsub))] = 0.0f;
-        }
-        if (l < 32) ccnt[l] = 0;
-        lds_fence();
-        // the encode kernel's B operand: lane (r, h) holds x~[r][h*8KS + 8ks + j] = f16(sigma x)
-        half8 bf[KS];
-        float xx = 0.0f;
-#pragma unroll
-        for (int ks = 0; ks < KS; ++ks) {
-            const u32x4 u = frag(xf + r * XP + h * 8 * KS + 8 * ks, sig1);
-            bf[ks] = __builtin_bit_cast(half8, u);
-            xx = dot2_self(u[0], xx); xx = dot2_self(u[1], xx);
-            xx = dot2_self(u[2], xx); xx = dot2_self(u[3], xx);
-        }
-        xx += __shfl_xor(xx, 32);
-        // all 256 unpacked scores of the lane's row half, one MFMA sweep
-        floatx16 acc[8];
-        constexpr int NCB = (V & 2048) ? 1 : 8;
-#pragma unroll
-        for (int cb = 0; cb < NCB; ++cb) {
-#pragma unroll
-            for (int qq = 0; qq < 4; ++qq) {
-                const float4 hv = *reinterpret_cast<const float4*>(hb + cb * 32 + 8 * qq + 4 * h);
-                acc[cb][4 * qq + 0] = hv.x; acc[cb][4 * qq + 1] = hv.y;
-                acc[cb][4 * qq + 2] = hv.z; acc[cb][4 * qq + 3] = hv.w;
-            }
-        }
-#pragma unroll
-        for (int ks = 0; ks < KS; ++ks)
-#pragma unroll
-            for (int cb = 0; cb < NCB; ++cb)
-                acc[cb] = __builtin_amdgcn_mfma_f32_32x32x16_f16(aa[cb][ks], bf[ks], acc[cb], 0, 0, 0);
-        float t1 = -INFINITY;
-#pragma unroll
-        for (int cb = 0; cb < NCB; ++cb)
-#pragma unroll
-            for (int i = 0; i < 16; ++i) t1 = fmaxf(t1, acc[cb][i]);
-        t1 = fmaxf(t1, __shfl_xor(t1, 32));
-        const float Xs = (__builtin_amdgcn_sqrtf(xx) * (1.0f + 1e-5f) + xs_eta) * (1.0f + 9.765625e-4f);
-        const float W = bm.y * Xs + bm.z;
-        const float thr = t1 - W;
-        const bool bad = !(Xs < 65000.0f) || !isfinite(t1) || !isfinite(W);
-#pragma unroll
-        for (int cb = 0; cb < NCB; ++cb) {
-#pragma unroll
-            for (int i = 0; i < 16; ++i) {
-                if (!bad && acc[cb][i] >= thr) {
-                    const int slot = atomicAdd(&ccnt[r], 1);
-                    if (slot < kFCap) cand[r * kFCap + slot] = cb * 32 + (i & 3) + 8 * (i >> 2) + 4 * h;
-                }
-            }
-        }
-        lds_fence();
-        // canonical chains: lane (r, h) takes every other candidate of row r
-        float bs = INFINITY;
-        int bk = 256;
-        const float* xr = xf + r * XP;
-        auto exact = [&](int k) __attribute__((always_inline)) {
-            const float* c = cl + k * CP;
-            float dot = 0.0f;
-            for (int t = 0; t < dsub; t += 4) {
-                const f32x4 cv = *reinterpret_cast<const f32x4*>(c + t);
-                const f32x4 xv = *reinterpret_cast<const f32x4*>(xr + t);
-                dot = __builtin_fmaf(xv.x, cv.x, dot);
-                dot = __builtin_fmaf(xv.y, cv.y, dot);
-                dot = __builtin_fmaf(xv.z, cv.z, dot);
-                dot = __builtin_fmaf(xv.w, cv.w, dot);
-            }
-            const float sc = __builtin_fmaf(-2.0f, dot, cnm[k]);
-            if (sc < bs || (sc == bs && k < bk)) { bs = sc; bk = k; }
-        };
-        if constexpr ((V & 512) != 0) {  // instrumentation: rows scanned whole, candidates total
-            if (h == 0 && r < cntb) {
-                int2* cc = const_cast<int2*>(counts) + blockIdx.x;
-                if (bad || ccnt[r] > kFCap) atomicAdd(&cc->x, 1 << 16);
-                atomicAdd(&cc->x, 1);
-                atomicAdd(&cc->y, ccnt[r] << 8);
-            }
-        }
-        if (r < cntb && !(V & 1024)) {
-            const int nc = ccnt[r];
-            if (bad || nc > kFCap) {
-                for (int k = h; k < 256; k += 2) exact(k);
-            } else {
-                for (int j = h; j < nc; j += 2) exact(cand[r * kFCap + j]);
-            }
-        }
-        const float os = __shfl_xor(bs, 32);
-        const int ok = __shfl_xor(bk, 32);
-        if (os < bs || (os == bs && ok < bk)) { bs = os; bk = ok; }
-        if (h == 0 && r < cntb) codesT[(int64_t)m * n + r0 + rowl] = (uint8_t)((bs < INFINITY) ? bk : 0);
-        lds_fence();
-    }
-}
-
-// Full items, high-occupancy form (the library default; V&65536 selects the kernel above):
-// the same filter re-run and candidate chains, but without the fp32 codebook in LDS, so two
-// workgroups of 4 waves fit a CU.  The f16 A operands come straight from the prepared image
-// (fragment order, one 16-B load per lane, L2-resident), the scores are computed twice (a
-// max pass for the window, then a pass that collects the candidates: MFMAs are cheap here),
-// and the canonical chains read the centroid rows from memory.  Grid: kF2Slices workgroups
-// per encode workgroup's list; wave w of slice s takes batches s*4 + w, s*4 + w + 4*kF2Slices, ...
-constexpr int kF2Slices = 2;
-
-template <int KS>
-constexpr int full2_smem_bytes() {
-    return 256 * 4 + kFWaves * (32 * (16 * KS + 4) * 4 + 32 * kFCap * 4 + 32 * 4);
-}
-
-template <int KS, int DS>
-__global__ __launch_bounds__(kFWaves * 64) __attribute__((amdgpu_waves_per_eu(2))) void pq_resolve_full2_kernel(
-    const float* __restrict__ x, int64_t n, int d, int M, int dsub_in, int64_t rows_per_wg, unsigned enc_grid,
-    const float* __restrict__ C, const float* __restrict__ cn, const half8* __restrict__ img,
-    const float* __restrict__ hinit, const float4* __restrict__ bnd, uint8_t* __restrict__ codesT,
-    const uint2* __restrict__ items, const int2* __restrict__ counts) {
-    constexpr int DP = 16 * KS;  // padded dsub
-    constexpr int XP = DP + 4;   // floats per staged x row
-    constexpr int NL = 2 * KS;   // 16-B loads per lane per batch (32 rows of <= DP floats)
-    constexpr int FR = 8 * KS * 64;
-    const int dsub = DS > 0 ? DS : dsub_in;
-    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-    float* hb = reinterpret_cast<float*>(smem);
-    const int tid = threadIdx.x;
-    const int w = __builtin_amdgcn_readfirstlane(tid >> 6), l = tid & 63;
-    const int r = l & 31, h = l >> 5;
-    float* xf = reinterpret_cast<float*>(smem + 256 * 4 + w * (32 * XP * 4 + 32 * kFCap * 4 + 32 * 4));
-    int* cand = reinterpret_cast<int*>(xf + 32 * XP);
-    int* ccnt = cand + 32 * kFCap;
-
-    const unsigned b = blockIdx.x / kF2Slices, sl = blockIdx.x % kF2Slices;
-    int m;
-    int64_t chunk;
-    wg_coords_of(b, enc_grid, M, m, chunk);
-    const int64_t r0 = chunk * rows_per_wg;
-    const int64_t r1 = min(n, r0 + rows_per_wg);
-    if (r0 >= r1) return;
-    const int nrows = (int)(r1 - r0);
-    const int nf = counts[b].y;
-    if (nf == 0) return;
-    hb[tid] = hinit[(int64_t)m * 256 + tid];
-    __syncthreads();
-
-    const float4 bm = bnd[m];
-    const float xs_eta = 5.9604645e-8f * sqrtf((float)dsub);
-    const float* cnm = cn + (int64_t)m * 256;
-    const float* Cm = C + (int64_t)m * 256 * dsub;
-    const half8* im = img + (int64_t)m * FR;
-    const int q = dsub >> 2;
-    const int nld = (32 * q + 63) >> 6;
-    const uint2* list = items + (int64_t)m * n + r0;
-    const float* xsub = x + r0 * d + (int64_t)m * dsub;
-    const int nbat = (nf + 31) >> 5;
-
-    auto frag = [&](const float* src) __attribute__((always_inline)) {
-        return cvt8_scaled(*reinterpret_cast<const f32x4*>(src), *reinterpret_cast<const f32x4*>(src + 4), bm.x);
-    };
-
-    for (int bt = (int)sl * kFWaves + w; bt < nbat; bt += kF2Slices * kFWaves) {
-        const int first = bt * 32;
-        const int cntb = min(32, nf - first);
-        int rowl = 0;
-        if (l < cntb) rowl = (int)list[nrows - 1 - (first + l)].x;
-        f32x4 v[NL];
-#pragma unroll
-        for (int j = 0; j < NL; ++j) {
-            const int c = j * 64 + l;
-            const int row = c / q, col = c - row * q;
-            const int src = __shfl(rowl, min(row, 31));
-            const bool ok = j < nld && row < cntb;
-            v[j] = *reinterpret_cast<const f32x4*>(xsub + (ok ? (int64_t)src * d + 4 * col : 0));
-        }
-#pragma unroll
-        for (int j = 0; j < NL; ++j) {
-            const int c = j * 64 + l;
-            const int row = c / q, col = c - row * q;
-            if (j < nld && row < 32) *reinterpret_cast<f32x4*>(xf + row * XP + 4 * col) = v[j];
-        }
-        if (DS == 0 || DS != DP)
-            for (int e = l; e < 32 * (DP - dsub); e += 64) {
-                const int row = e / (DP - dsub);
-                xf[row * XP + dsub + (e - row * (DP - dsub))] = 0.0f;
-            }
-        if (l < 32) ccnt[l] = 0;
-        lds_fence();
-        half8 bf[KS];
-        float xx = 0.0f;
-#pragma unroll
-        for (int ks = 0; ks < KS; ++ks) {
-            const u32x4 u = frag(xf + r * XP + h * 8 * KS + 8 * ks);
-            bf[ks] = __builtin_bit_cast(half8, u);
-            xx = dot2_self(u[0], xx); xx = dot2_self(u[1], xx);
-            xx = dot2_self(u[2], xx); xx = dot2_self(u[3], xx);
-        }
-        xx += __shfl_xor(xx, 32);
-        // an opaque zero tied to the batch keeps the image loads inside the loop (hoisted, the
-        // 8 * KS fragments would need 4 * 8 * KS registers)
-        const int oz = __builtin_amdgcn_readfirstlane(bt) >> 30;
-        const half8* imb = im + oz;
-        const float* hbb = hb + oz;  // (same for the accumulator init: 128 values per lane)
-        auto scores = [&](int cb) __attribute__((always_inline)) {
-            half8 a[KS];
-#pragma unroll
-            for (int ks = 0; ks < KS; ++ks) a[ks] = imb[(cb * KS + ks) * 64 + l];
-            floatx16 acc;
-#pragma unroll
-            for (int qq = 0; qq < 4; ++qq) {
-                const float4 hv = *reinterpret_cast<const float4*>(hbb + cb * 32 + 8 * qq + 4 * h);
-                acc[4 * qq + 0] = hv.x; acc[4 * qq + 1] = hv.y;
-                acc[4 * qq + 2] = hv.z; acc[4 * qq + 3] = hv.w;
-            }
-#pragma unroll
-            for (int ks = 0; ks < KS; ++ks) acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(a[ks], bf[ks], acc, 0, 0, 0);
-            return acc;
-        };
-        float t1 = -INFINITY;
-#pragma unroll 1
-        for (int cb = 0; cb < 8; ++cb) {
-            const floatx16 acc = scores(cb);
-#pragma unroll
-            for (int i = 0; i < 16; ++i) t1 = fmaxf(t1, acc[i]);
-        }
-        t1 = fmaxf(t1, __shfl_xor(t1, 32));
-        const float Xs = (__builtin_amdgcn_sqrtf(xx) * (1.0f + 1e-5f) + xs_eta) * (1.0f + 9.765625e-4f);
-        const float W = bm.y * Xs + bm.z;
-        const float thr = t1 - W;
-        const bool bad = !(Xs < 65000.0f) || !isfinite(t1) || !isfinite(W);
-#pragma unroll 1
-        for (int cb = 0; cb < 8; ++cb) {
-            const floatx16 acc = scores(cb);
-#pragma unroll
-            for (int i = 0; i < 16; ++i) {
-                if (!bad && acc[i] >= thr) {
-                    const int slot = atomicAdd(&ccnt[r], 1);
-                    if (slot < kFCap) cand[r * kFCap + slot] = cb * 32 + (i & 3) + 8 * (i >> 2) + 4 * h;
-                }
-            }
-        }
-        lds_fence();
-        float bs = INFINITY;
-        int bk = 256;
-        const float* xr = xf + r * XP;
-        auto exact = [&](int k) __attribute__((always_inline)) {
-            const float* c = Cm + (int64_t)k * dsub;
-            float dot = 0.0f;
-            if constexpr (DS > 0 && DS % 8 == 0) {
-                // centroid row from memory, half a row in flight at a time; the x row is read
-                // from LDS per candidate (an opaque zero keeps those reads from being hoisted
-                // out of the candidate loop, where they would need 4 * DS / 4 registers)
-                const float* xk = xr + (__builtin_amdgcn_readfirstlane(k) >> 30);
-#pragma unroll
-                for (int hf = 0; hf < 2; ++hf) {
-                    f32x4 cv[DS / 8];
-#pragma unroll
-                    for (int t = 0; t < DS / 8; ++t) cv[t] = *reinterpret_cast<const f32x4*>(c + hf * (DS / 2) + 4 * t);
-#pragma unroll
-                    for (int t = 0; t < DS / 8; ++t) {
-                        const f32x4 xv = *reinterpret_cast<const f32x4*>(xk + hf * (DS / 2) + 4 * t);
-                        dot = __builtin_fmaf(xv.x, cv[t].x, dot);
-                        dot = __builtin_fmaf(xv.y, cv[t].y, dot);
-                        dot = __builtin_fmaf(xv.z, cv[t].z, dot);
-                        dot = __builtin_fmaf(xv.w, cv[t].w, dot);
-                    }
-                }
-            } else {
-                for (int t = 0; t < dsub; t += 4) {
-                    const f32x4 cv = *reinterpret_cast<const f32x4*>(c + t);
-                    const f32x4 xv = *reinterpret_cast<const f32x4*>(xr + t);
-                    dot = __builtin_fmaf(xv.x, cv.x, dot);
-                    dot = __builtin_fmaf(xv.y, cv.y, dot);
-                    dot = __builtin_fmaf(xv.z, cv.z, dot);
-                    dot = __builtin_fmaf(xv.w, cv.w, dot);
-                }
-            }
-            const float sc = __builtin_fmaf(-2.0f, dot, cnm[k]);
-            if (sc < bs || (sc == bs && k < bk)) { bs = sc; bk = k; }
-        };
-        if (r < cntb) {
-            const int nc = ccnt[r];
-            if (bad || nc > kFCap) {
-                for (int k = h; k < 256; k += 2) exact(k);
-            } else {
-                for (int j = h; j < nc; j += 2) exact(cand[r * kFCap + j]);
-            }
-        }
-        const float os = __shfl_xor(bs, 32);
-        const int ok = __shfl_xor(bk, 32);
-        if (os < bs || (os == bs && ok < bk)) { bs = os; bk = ok; }
-        if (h == 0 && r < cntb) codesT[(int64_t)m * n + r0 + rowl] = (uint8_t)((bs < INFINITY) ? bk : 0);
-        lds_fence();
-    }
 }
 
 // Merged resolve (the library default): one launch settles a workgroup's full items and the
@@ -1522,7 +632,7 @@ constexpr int kGcCap = 4096;
 template <int KS>
 constexpr int merged_smem_bytes() {
     return (merged_gc<KS>() ? 0 : 256 * 16 * KS * 4) + 2 * 256 * 4 + 16 + kMWaves * (32 * (16 * KS + 4) * 4) +
-           (merged_gc<KS>() && MIVQ_GC_LIST ? kMWaves * (32 * 8 + kGcCap * 2) : 0);
+           (merged_gc<KS>() ? kMWaves * (32 * 8 + kGcCap * 2) : 0);
 }
 
 // float -> uint32 whose unsigned order is the float order (-0 == +0; NaN above everything)
@@ -1531,10 +641,7 @@ __device__ __forceinline__ uint32_t ord_key(float s) {
     return s != s ? 0xFFFFFFFFu : (u & 0x80000000u) ? ~u : (u | 0x80000000u);
 }
 
-// V (profiling, tools/cs_variants.hip): 1 << 21 skips the full batches, 1 << 22 the pair
-// batches, 1 << 23 does the gathers only (no MFMA, no chains), 1 << 24 skips the full
-// batches' chains, 1 << 25 their candidate collection and chains (wrong codes).
-template <int KS, int DS, int V = 0>
+template <int KS, int DS>
 __global__ __launch_bounds__(kMWaves * 64) __attribute__((amdgpu_waves_per_eu(1, 1))) void pq_resolve_merged_kernel(
     const float* __restrict__ x, int64_t n, int d, int M, int dsub_in, int64_t rows_per_wg,
     const float* __restrict__ C, const float* __restrict__ cn, const half8* __restrict__ img,
@@ -1622,7 +729,7 @@ __global__ __launch_bounds__(kMWaves * 64) __attribute__((amdgpu_waves_per_eu(1,
         const int sw = GC ? 0 : cswz<KS>(k);
         // the centroid row in two halves (register budget: the pair loop holds a prefetched
         // gather next to the row)
-        constexpr int NH = (GC && MIVQ_GC_WHOLE_ROW) ? NQ : (NQ + 1) / 2;
+        constexpr int NH = (NQ + 1) / 2;
         float dot = 0.0f;
 #pragma unroll
         for (int t0 = 0; t0 < NQ; t0 += NH) {
@@ -1793,10 +900,6 @@ __global__ __launch_bounds__(kMWaves * 64) __attribute__((amdgpu_waves_per_eu(1,
         const float W = bm.y * Xs + bm.z;
         const float thr = t1 - W;
         const bool bad = !(Xs < 65000.0f) || !isfinite(t1) || !isfinite(W);
-        if constexpr ((V & (1 << 25)) != 0) {
-            if (h == 0 && r < cntb) codesT[(int64_t)m * n + r0 + rowl] = (uint8_t)(__float_as_uint(thr) & 0xFF);
-            return;
-        }
         // this lane's centroids inside the window as a 128-bit mask (4 words of two centroid
         // blocks; register-only, no per-value LDS stores), then their canonical chains in
         // increasing k, one loop for all of them; a row the window cannot vouch for takes
@@ -1809,7 +912,7 @@ __global__ __launch_bounds__(kMWaves * 64) __attribute__((amdgpu_waves_per_eu(1,
             for (int i = 0; i < 32; ++i) mm |= acc[2 * q2 + (i >> 4)][i & 15] >= thr ? (1u << i) : 0u;
             wm[q2] = bad ? 0xFFFFFFFFu : mm;
         }
-        if constexpr (GC && MIVQ_GC_LIST && DS > 0 && (V & (1 << 24)) == 0) {
+        if constexpr (GC && DS > 0) {
             // candidate list: lane prefix of the candidate counts, entries (row << 8) | k
             const int cnt = r < cntb ? __popc(wm[0]) + __popc(wm[1]) + __popc(wm[2]) + __popc(wm[3]) : 0;
             int inc = cnt;
@@ -1839,7 +942,7 @@ __global__ __launch_bounds__(kMWaves * 64) __attribute__((amdgpu_waves_per_eu(1,
                     if (base + l < T) {
                         const int e = glist[base + l];
                         const int rr = e >> 8, k = e & 0xFF;
-                        const float sc = chain_gc(std::integral_constant<int, (DS > 128 ? MIVQ_GC_LIST_NC : 1)>{}, xf + rr * XP, k);
+                        const float sc = chain_gc(std::integral_constant<int, (DS > 128 ? kGcListNc : 1)>{}, xf + rr * XP, k);
                         atomicMin(&gkeys[rr], ((unsigned long long)ord_key(sc) << 32) | (unsigned)k);
                     }
                 }
@@ -1857,7 +960,7 @@ __global__ __launch_bounds__(kMWaves * 64) __attribute__((amdgpu_waves_per_eu(1,
         auto take = [&](float sc, int k) __attribute__((always_inline)) {
             if (sc < bs || (sc == bs && k < bk)) { bs = sc; bk = k; }
         };
-        if (r < cntb && !(V & (1 << 24))) {
+        if (r < cntb) {
             f32x4 xv[GC ? 1 : NQ];
             if constexpr (DS > 0 && !GC) load_row(xr, xv);
             while ((wm[0] | wm[1] | wm[2] | wm[3]) != 0u) {
@@ -1912,8 +1015,7 @@ __global__ __launch_bounds__(kMWaves * 64) __attribute__((amdgpu_waves_per_eu(1,
     // Full batches first (claimed from ctr[0]; their A operands take 192 registers, so their
     // gathers are not prefetched), then pair batches (claimed from ctr[1]) with the next pair
     // batch's gather in flight while the current one is computed.
-    if (!(V & (1 << 21)))
-        for (;;) {
+    for (;;) {
             int b = 0;
             if (l == 0) b = atomicAdd(&ctr[0], 1);
             b = __builtin_amdgcn_readfirstlane(__shfl(b, 0));
@@ -1931,10 +1033,9 @@ __global__ __launch_bounds__(kMWaves * 64) __attribute__((amdgpu_waves_per_eu(1,
                     for (int ks = 0; ks < KS; ++ks) aa[cb][ks] = im[(cb * KS + ks) * 64 + l];
             }
             gather_commit(v);
-            if (!(V & (1 << 23))) full_batch(aa, cntb, (int)it.x);
+            full_batch(aa, cntb, (int)it.x);
             lds_fence();  // the tile is rewritten by the next commit
         }
-    if (V & (1 << 22)) return;
     // pair batches: the first one per wave is static (b = w), the rest are claimed from ctr[1]
     int b = w, cntb = 0;
     uint2 it = make_uint2(0u, 0u);
@@ -1953,7 +1054,7 @@ __global__ __launch_bounds__(kMWaves * 64) __attribute__((amdgpu_waves_per_eu(1,
         __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
         gather_commit(vc);
         gather_issue(cntn, (int)itn.x, vn);  // cntn <= 0: every lane reads row 0 (discarded)
-        if (!(V & (1 << 23))) pair_batch(cntb, it);
+        pair_batch(cntb, it);
         lds_fence();  // the tile is rewritten by the next commit
         b = bn;
         it = itn;
@@ -2044,12 +1145,6 @@ int64_t pick_chunks(int64_t n, int d, int M, int cus, int nw) {
         const double cost = (double)ceil_div(c * M, (int64_t)cus) / (double)c;
         if (cost < best_cost * (1.0 - 1e-9)) { best_cost = cost; best = c; }
     }
-#ifdef MIVQ_CS_CHUNK_MULT
-    best = std::min<int64_t>(best * MIVQ_CS_CHUNK_MULT, std::max<int64_t>(best, ceil_div(n, 32 * nw)));
-#endif
-#ifdef MIVQ_CS_FORCE_CHUNKS
-    best = std::max<int64_t>(cmin, MIVQ_CS_FORCE_CHUNKS);
-#endif
     return best;
 }
 
@@ -2069,59 +1164,43 @@ int cs_layout(int dsub) {
     }
 }
 
-template <int KS, int V>
+template <int KS>
 hipError_t launch_pq_encode_cs_v(const float* x, int64_t n, int d, int M, int dsub, const float* C, const float* cn,
                                  const void* img, const float* hinit, const void* bnd, const void* pd, const void* bnd2,
-                                 uint8_t* codesT, void* items, void* counts, void* pinfo, hipStream_t st) {
+                                 uint8_t* codesT, void* items, void* counts, hipStream_t st) {
     const int smem = cs_smem_bytes(KS, dsub);
     const int layout = cs_layout(dsub);
     constexpr int NW = cs_waves(KS);
-    auto kern = layout == 1 ? pq_encode_cs_kernel<KS, 1, V, 0, NW>
-              : layout == 3 ? pq_encode_cs_kernel<KS, 3, V, 0, NW> : pq_encode_cs_kernel<KS, 0, V, 0, NW>;
-#ifndef MIVQ_CS_D64_WAVES
-#define MIVQ_CS_D64_WAVES 16
-#endif
-#ifndef MIVQ_CS_D48_WAVES
-#define MIVQ_CS_D48_WAVES 16
-#endif
-#ifndef MIVQ_CS_D96_WAVES
-#define MIVQ_CS_D96_WAVES 12
-#endif
+    auto kern = layout == 1 ? pq_encode_cs_kernel<KS, 1, 0, NW>
+              : layout == 3 ? pq_encode_cs_kernel<KS, 3, 0, NW> : pq_encode_cs_kernel<KS, 0, 0, NW>;
     int nw_launch = NW, smem_launch = smem;
-    if constexpr (KS == 6) {
-        if (dsub == 96) {
-            kern = pq_encode_cs_kernel<6, 3, V, 96, MIVQ_CS_D96_WAVES>;
-            nw_launch = MIVQ_CS_D96_WAVES;
-            smem_launch = smem + (MIVQ_CS_D96_WAVES - NW) * 32 * (32 * KS + 16);
-        }
+    // specialised shapes (addresses and load counts folded; waves per shape measured)
+    if constexpr (KS == 6) {  // D = 1536, M = 16: the headline
+        if (dsub == 96) kern = pq_encode_cs_kernel<6, 3, 96, 12>;
     }
     if constexpr (KS == 3) {  // D = 1536, M = 32 (the OPQ32 / PQ32 shape of BASELINE config #3)
         if (dsub == 48) {
-            kern = pq_encode_cs_kernel<3, 3, V, 48, MIVQ_CS_D48_WAVES>;
-            nw_launch = MIVQ_CS_D48_WAVES;
-            smem_launch = smem + (MIVQ_CS_D48_WAVES - NW) * 32 * (32 * KS + 16);
+            constexpr int NW48 = 16;
+            kern = pq_encode_cs_kernel<3, 3, 48, NW48>;
+            nw_launch = NW48;
+            smem_launch = smem + (NW48 - NW) * 32 * (32 * KS + 16);
         }
     }
     if constexpr (KS == 4) {  // D = 1024, M = 16 (BASELINE config #5)
         if (dsub == 64) {
-            kern = pq_encode_cs_kernel<4, 1, V, 64, MIVQ_CS_D64_WAVES>;
-            nw_launch = MIVQ_CS_D64_WAVES;
-            smem_launch = smem + (MIVQ_CS_D64_WAVES - NW) * 32 * (32 * KS + 16);
+            constexpr int NW64 = 16;
+            kern = pq_encode_cs_kernel<4, 1, 64, NW64>;
+            nw_launch = NW64;
+            smem_launch = smem + (NW64 - NW) * 32 * (32 * KS + 16);
         }
     }
-#ifndef MIVQ_CS_WIDE_WAVES
-#define MIVQ_CS_WIDE_WAVES 8
-#endif
-#ifndef MIVQ_CS_WIDE_WAVES_KS8
-#define MIVQ_CS_WIDE_WAVES_KS8 MIVQ_CS_WIDE_WAVES
-#endif
     // wide subspaces with dsub == 16 KS (128, 160, 192): the tile filled in two K halves, so 8
     // waves fit next to the image instead of 4 (KH = 2 above)
-    if constexpr (KS >= 8 && KS % 2 == 0 && MIVQ_CS_WIDE_WAVES > 0 && (V & (1 << 21)) == 0) {
+    if constexpr (KS >= 8 && KS % 2 == 0) {
         if (dsub == 16 * KS) {
-            constexpr int KT = KS / 2, NWW = KS == 8 ? MIVQ_CS_WIDE_WAVES_KS8 : MIVQ_CS_WIDE_WAVES;
+            constexpr int KT = KS / 2, NWW = 8;
             constexpr int LH = (4 * KT == 24 || 4 * KT == 12) ? 3 : (4 * KT == 16 || 4 * KT == 32) ? 1 : 0;
-            kern = pq_encode_cs_kernel<KS, LH, V, 16 * KS, NWW, 2>;
+            kern = pq_encode_cs_kernel<KS, LH, 16 * KS, NWW, 2>;
             nw_launch = NWW;
             smem_launch = 8 * KS * 64 * 16 + NWW * 32 * (32 * KT + 16) + 2 * 256 * 4 + 16;
         }
@@ -2132,71 +1211,28 @@ hipError_t launch_pq_encode_cs_v(const float* x, int64_t n, int d, int M, int ds
     const int64_t chunks = pick_chunks(n, d, M, cus, nw_launch);
     const int64_t R = align_up(ceil_div(n, chunks), (int64_t)32);
     const int64_t grid = ceil_div(n, R) * M;
-    // V & (1 << 20): the round-1 resolve (pair window in the pair kernel, separate full-item
-    // and pair kernels), kept for A/B profiling
-    constexpr bool legacy = (V & (1 << 20)) != 0;
-    const float2* pdw = legacy ? nullptr : static_cast<const float2*>(pd);
     hipLaunchKernelGGL(kern, dim3((unsigned)grid), dim3(nw_launch * 64), smem_launch, st, x, n, d, M, dsub, R, C, cn,
                        static_cast<const half8*>(img), hinit, static_cast<const float4*>(bnd), codesT,
-                       static_cast<uint2*>(items), static_cast<int2*>(counts), static_cast<float2*>(pinfo), pdw,
+                       static_cast<uint2*>(items), static_cast<int2*>(counts), static_cast<const float2*>(pd),
                        static_cast<const float4*>(bnd2));
     e = hipGetLastError();
-    if (e != hipSuccess || ((V & 1) && !(V & 512))) return e;
-    if constexpr (!legacy) {
-        constexpr int msmem = merged_smem_bytes<KS>();
-        static_assert(msmem <= 160 * 1024, "merged resolve LDS");
-        // DS specialisations: the row held in registers for the chains (exact_reg); wide
-        // subspaces with dsub == 16 KS as well (their chains read C from L2)
-        constexpr bool wide_ds = KS >= 8 && KS % 2 == 0 && MIVQ_GC_DS;
-        auto mkern = (KS == 6 && dsub == 96)   ? pq_resolve_merged_kernel<KS, (KS == 6 ? 96 : 0), V>
-                     : (KS == 4 && dsub == 64) ? pq_resolve_merged_kernel<KS, (KS == 4 ? 64 : 0), V>
-                     : (KS == 3 && dsub == 48) ? pq_resolve_merged_kernel<KS, (KS == 3 ? 48 : 0), V>
-                     : (wide_ds && dsub == 16 * KS) ? pq_resolve_merged_kernel<KS, (wide_ds ? 16 * KS : 0), V>
-                                               : pq_resolve_merged_kernel<KS, 0, V>;
-        e = hipFuncSetAttribute((const void*)mkern, hipFuncAttributeMaxDynamicSharedMemorySize, msmem);
-        if (e != hipSuccess) return e;
-        hipLaunchKernelGGL(mkern, dim3((unsigned)grid), dim3(kMWaves * 64), msmem, st, x, n, d, M, dsub, R, C, cn,
-                           static_cast<const half8*>(img), hinit, static_cast<const float4*>(bnd), codesT,
-                           static_cast<const uint2*>(items), static_cast<const int2*>(counts));
-        return hipGetLastError();
-    } else {
-    constexpr int rsmem = resolve_smem_bytes<KS>();
-    auto rkern = pq_resolve_cs_kernel<KS, V>;
-    e = hipFuncSetAttribute((const void*)rkern, hipFuncAttributeMaxDynamicSharedMemorySize, rsmem);
     if (e != hipSuccess) return e;
-    // full items through pq_resolve_full_kernel (filter re-run + candidate chains): 1.5-2 %
-    // faster end to end than the pair kernel's 256-wide scans (interleaved A/B, 1M x 1536);
-    // V&256 restores the scans
-    constexpr bool mfma_full = (V & 256) == 0;
-    if (mfma_full && !(V & 65536) && !(V & 512)) {
-        constexpr int fsmem = full2_smem_bytes<KS>();
-        auto fkern = (KS == 6 && dsub == 96) ? pq_resolve_full2_kernel<KS, (KS == 6 ? 96 : 0)>
-                                             : pq_resolve_full2_kernel<KS, 0>;
-        e = hipFuncSetAttribute((const void*)fkern, hipFuncAttributeMaxDynamicSharedMemorySize, fsmem);
-        if (e != hipSuccess) return e;
-        hipLaunchKernelGGL(fkern, dim3((unsigned)(grid * kF2Slices)), dim3(kFWaves * 64), fsmem, st, x, n, d, M, dsub,
-                           R, (unsigned)grid, C, cn, static_cast<const half8*>(img), hinit,
-                           static_cast<const float4*>(bnd), codesT, static_cast<const uint2*>(items),
-                           static_cast<const int2*>(counts));
-        e = hipGetLastError();
-        if (e != hipSuccess || (V & 1)) return e;
-    } else if (mfma_full) {
-        constexpr int fsmem = full_smem_bytes<KS>();
-        auto fkern = pq_resolve_full_kernel<KS, V>;
-        e = hipFuncSetAttribute((const void*)fkern, hipFuncAttributeMaxDynamicSharedMemorySize, fsmem);
-        if (e != hipSuccess) return e;
-        hipLaunchKernelGGL(fkern, dim3((unsigned)grid), dim3(kFWaves * 64), fsmem, st, x, n, d, M, dsub, R, C, cn,
-                           hinit, static_cast<const float4*>(bnd), codesT, static_cast<const uint2*>(items),
-                           static_cast<const int2*>(counts));
-        e = hipGetLastError();
-        if (e != hipSuccess || (V & 1)) return e;  // V&513: the instrumented full kernel alone
-    }
-    hipLaunchKernelGGL(rkern, dim3((unsigned)grid), dim3(kRWaves * 64), rsmem, st, x, n, d, M, dsub, R, C, cn, codesT,
-                       static_cast<const uint2*>(items), static_cast<const int2*>(counts), mfma_full ? 0 : 1,
-                       (V & 32768) ? nullptr : static_cast<const float2*>(pd), static_cast<const float4*>(bnd2),
-                       static_cast<const float2*>(pinfo));
+    constexpr int msmem = merged_smem_bytes<KS>();
+    static_assert(msmem <= 160 * 1024, "merged resolve LDS");
+    // DS specialisations: the row held in registers for the chains (exact_reg); wide
+    // subspaces with dsub == 16 KS as well (their chains read C from L2)
+    constexpr bool wide_ds = KS >= 8 && KS % 2 == 0;
+    auto mkern = (KS == 6 && dsub == 96)   ? pq_resolve_merged_kernel<KS, (KS == 6 ? 96 : 0)>
+                 : (KS == 4 && dsub == 64) ? pq_resolve_merged_kernel<KS, (KS == 4 ? 64 : 0)>
+                 : (KS == 3 && dsub == 48) ? pq_resolve_merged_kernel<KS, (KS == 3 ? 48 : 0)>
+                 : (wide_ds && dsub == 16 * KS) ? pq_resolve_merged_kernel<KS, (wide_ds ? 16 * KS : 0)>
+                                           : pq_resolve_merged_kernel<KS, 0>;
+    e = hipFuncSetAttribute((const void*)mkern, hipFuncAttributeMaxDynamicSharedMemorySize, msmem);
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(mkern, dim3((unsigned)grid), dim3(kMWaves * 64), msmem, st, x, n, d, M, dsub, R, C, cn,
+                       static_cast<const half8*>(img), hinit, static_cast<const float4*>(bnd), codesT,
+                       static_cast<const uint2*>(items), static_cast<const int2*>(counts));
     return hipGetLastError();
-    }
 }
 
 // (at most ceil(n / (32 nw)) row chunks per subspace; nw >= kWideWaves)
@@ -2204,14 +1240,13 @@ size_t cs_counts_bytes(int64_t n, int M) { return (size_t)ceil_div(n, 32 * kWide
 
 hipError_t launch_pq_encode_cs(int KS, const float* x, int64_t n, int d, int M, int dsub, const float* C,
                                const float* cn, const void* img, const float* hinit, const void* bnd, const void* pd,
-                               const void* bnd2, uint8_t* codesT, void* items, void* counts, void* pinfo,
-                               uint8_t* codes, hipStream_t st) {
+                               const void* bnd2, uint8_t* codesT, void* items, void* counts, uint8_t* codes,
+                               hipStream_t st) {
     hipError_t e = hipErrorInvalidValue;
     switch (KS) {
 #define MIVQ_CS_CASE(k)                                                                                        \
     case k:                                                                                                    \
-        e = launch_pq_encode_cs_v<k, 0>(x, n, d, M, dsub, C, cn, img, hinit, bnd, pd, bnd2, codesT, items, counts, \
-                                        pinfo, st);                                                            \
+        e = launch_pq_encode_cs_v<k>(x, n, d, M, dsub, C, cn, img, hinit, bnd, pd, bnd2, codesT, items, counts, st); \
         break;
         MIVQ_CS_CASE(1) MIVQ_CS_CASE(2) MIVQ_CS_CASE(3) MIVQ_CS_CASE(4) MIVQ_CS_CASE(5) MIVQ_CS_CASE(6)
         MIVQ_CS_CASE(7) MIVQ_CS_CASE(8) MIVQ_CS_CASE(9) MIVQ_CS_CASE(10) MIVQ_CS_CASE(11) MIVQ_CS_CASE(12)

@@ -82,7 +82,7 @@ struct WaveTopK {
 // Merges per-part sorted lists laid out (parts, nq, k) into (nq, k); parts == 0 writes the
 // sentinel everywhere.  Defined in adc.hip.
 hipError_t launch_topk_merge(const float* pd, const uint32_t* pi, int parts, int64_t nq, int k, float* od,
-                             uint32_t* oi, hipStream_t st);
+                             uint32_t* oi, hipStream_t st, const int* qlist = nullptr, const int* qcount = nullptr);
 
 // Tiled top-k (ivf.hip): a key-block producer + segmented top-k + running merge.  The
 // workspace of flat_tiled_workspace_bytes serves both launchers.

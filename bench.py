@@ -299,7 +299,9 @@ def adc_leg(X, C, codes, a, rank, world, dev, Q, k, gt_queries, reps=3, cpu=True
     search = lambda: sharded.sharded_adc_search(Q, C, codes, nbits, k, off)  # noqa: E731
     wall, dev_ms = timed(search, reps, 1, world, dev)
     ad, ai = search()
-    # the scan kernel alone (no LUT build, no exchange): the LDS roofline of adc_scan
+    # mivq_adc_search alone (no LUT build, no exchange): for M = 16 / 32 the filtered path
+    # (integer-LUT scan, exact fp32 re-rank + certificate, fp32 re-run of uncertified queries:
+    # DESIGN §3.3), every launch of it inside the timed call
     lut = _native.adc_lut(Q, C, nbits)
     _, scan_ms = timed(lambda: _native.adc_search(lut, codes, k, nbits, id_offset=off), reps, 1)
     gq = min(gt_queries, nq)
@@ -317,10 +319,14 @@ def adc_leg(X, C, codes, a, rank, world, dev, Q, k, gt_queries, reps=3, cpu=True
            f"recall@{k}": rec(gt, got), "recall_queries": gq,
            f"recall@{k}_decode_exact": rec(gt, dec), "topk_agreement_adc_vs_decode_exact": rec(dec, got),
            "gt": "exact L2 top-k over the raw vectors (mivq_flat_search, sharded + merged)",
-           "roofline": {"bound": "lds", "kernel": "adc_scan_kernel (per rank, LUT in LDS)",
+           "roofline": {"bound": "lds", "kernel": "mivq_adc_search (per rank: qstats + qtab + adc_qscan_kernel + "
+                                                   "adc_rerank_kernel + fp32 re-run of uncertified queries)",
                         "achieved": lds_bytes / (scan_ms * 1e-3) / 1e9, "peak": LDS_PEAK_GBS, "unit": "GB/s",
                         "frac": lds_bytes / (scan_ms * 1e-3) / 1e9 / LDS_PEAK_GBS, "scan_ms": scan_ms,
-                        "lds_bytes_per_query_row": M * 4}}
+                        "lds_bytes_per_query_row": M * 4,
+                        "note": "algorithmic bytes = one fp32 LUT entry per (query, row, subspace), the canonical "
+                                "ADC's work; the filtered scan itself reads 2-B integer entries (M * 2 B per "
+                                "(query, row) from LDS)"}}
     if cpu and rank == 0 and world == 1:
         O = _oracle()
         nqs = min(nq, 50)

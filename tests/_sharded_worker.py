@@ -39,6 +39,12 @@ def main():
             res[metric] = {"sharded_ids": ids.astype(np.int64).tolist(), "sharded_d": dists.tolist(),
                            "single_ids": i1.cpu().numpy().view(np.uint32).astype(np.int64).tolist(),
                            "single_d": d1.cpu().numpy().tolist()}
+        idx.save(out.parent / f"idx_{metric}")  # per-rank shard files, then a fresh index from them
+        idx2 = ShardedFlatIndex(ProductQuantizer(M=8, B=8))
+        idx2.load(out.parent / f"idx_{metric}")
+        ids2, dists2 = idx2.search_with_scores(Q, k)
+        if info.rank == 0:
+            res[metric]["reload_equal"] = bool(np.array_equal(ids2, ids) and np.array_equal(dists2, dists))
         big = idx.search_with_scores(Q[:3], 300)  # k > 256: the decode + exact path per shard
         if info.rank == 0:
             res[metric]["k300_ids"] = big[0].astype(np.int64).tolist()

@@ -76,6 +76,7 @@ def test_sharded_flat_index_two_ranks_one_gpu(dev, tmp_path):
         assert r["sharded_ids"] == r["single_ids"], metric
         assert np.array_equal(np.array(r["sharded_d"], np.float32), np.array(r["single_d"], np.float32)), metric
         assert r["k300_ids"] == r["k300_single_ids"], metric
+        assert r["reload_equal"], metric  # save / load of the per-rank shard files
     assert res["l2"]["sharded_ids"][0][:3] == [5, 17, 30008]  # exact duplicates: by id across the shards
 
 

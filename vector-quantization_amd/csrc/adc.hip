@@ -123,6 +123,8 @@ typedef float f32x4v __attribute__((ext_vector_type(4)));
 typedef __attribute__((address_space(3))) const f32x4v lds_f4;
 typedef unsigned int u32x4v __attribute__((ext_vector_type(4)));
 typedef __attribute__((address_space(3))) const u32x4v lds_u4;
+typedef unsigned int u32x2v __attribute__((ext_vector_type(2)));
+typedef __attribute__((address_space(3))) const u32x2v lds_u2;
 
 // Undoes the odd lanes' half order of lut_add<8> (identity for other QB).
 template <int QB>
@@ -143,10 +145,10 @@ __device__ __forceinline__ void lut_unswap(float (&dist)[QB], uint32_t par) {
 // 16-B loads issued one wave-step ahead, so the LDS lookups never wait on the code fetch
 // (MC = 0: 4-B code words loaded in the step that uses them).
 template <int R, int QB, int MC>
-__global__ __launch_bounds__(kScanWaves * 64) void adc_scan_kernel(
+__device__ __forceinline__ void adc_scan_block(
     const float* __restrict__ lut, int64_t nq, const uint8_t* __restrict__ codes, int64_t n, int M,
     int ksub, int k, int64_t id_offset, int64_t chunk_rows, float* __restrict__ part_d,
-    uint32_t* __restrict__ part_i, const int* __restrict__ qlist, const int* __restrict__ qcount) {
+    uint32_t* __restrict__ part_i, const int* __restrict__ qlist, const int* __restrict__ qcount, int64_t yb) {
     if constexpr (MC > 0) {
         M = 16 * MC;
         ksub = 256;
@@ -158,11 +160,11 @@ __global__ __launch_bounds__(kScanWaves * 64) void adc_scan_kernel(
     // QB separate 4-B reads)
     extern __shared__ __attribute__((aligned(16))) float tab[];
     const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
-    const int64_t q0 = (int64_t)blockIdx.y * QB;
+    const int64_t q0 = yb * QB;
     int nqb = (int)min<int64_t>(QB, nq - q0);
     if (qlist != nullptr) {
         const int cnt = *qcount;
-        if (q0 >= cnt) return;  // whole workgroup, before any barrier
+        if (q0 >= cnt) return;  // whole workgroup (the caller's loop ends too)
         nqb = (int)min<int64_t>(QB, cnt - q0);
     }
     const int64_t tab_elems = (int64_t)M * ksub;
@@ -294,6 +296,27 @@ __global__ __launch_bounds__(kScanWaves * 64) void adc_scan_kernel(
             const int e = r * 64 + lane;
             if (e < k) { od[e] = top[qq].d[r]; oi[e] = top[qq].id[r]; }
         }
+    }
+}
+
+// Query block blockIdx.y (fp32 scan of every query), or -- qlist, the re-run of the queries
+// the filtered search could not certify -- list slots blockIdx.y, + gridDim.y, ... while they
+// exist: a small grid whatever the count (0 failures: every workgroup returns at once).
+template <int R, int QB, int MC>
+__global__ __launch_bounds__(kScanWaves * 64) void adc_scan_kernel(
+    const float* __restrict__ lut, int64_t nq, const uint8_t* __restrict__ codes, int64_t n, int M,
+    int ksub, int k, int64_t id_offset, int64_t chunk_rows, float* __restrict__ part_d,
+    uint32_t* __restrict__ part_i, const int* __restrict__ qlist, const int* __restrict__ qcount) {
+    if (qlist == nullptr) {
+        adc_scan_block<R, QB, MC>(lut, nq, codes, n, M, ksub, k, id_offset, chunk_rows, part_d, part_i, qlist, qcount,
+                                  (int64_t)blockIdx.y);
+        return;
+    }
+    const int cnt = *qcount;
+    for (int64_t yb = blockIdx.y; yb * QB < cnt; yb += gridDim.y) {
+        adc_scan_block<R, QB, MC>(lut, nq, codes, n, M, ksub, k, id_offset, chunk_rows, part_d, part_i, qlist, qcount,
+                                  yb);
+        __syncthreads();  // the next block's table overwrites this one's
     }
 }
 
@@ -472,7 +495,10 @@ struct AdcQStat {
     int bad, pad;
 };
 
-__host__ __device__ constexpr int adc_qmax(int M) { return 32767 / M; }
+// Table entries: u16 per query (QMAX = 32767 / M), or u8 (QMAX = 255, E8: half the table
+// bytes again; unpacked to the u16 fields by two v_perm_b32 per dword).
+constexpr bool kAdcE8 = true;  // u8 entries (round 5: the u16 table measured no faster per call)
+__host__ __device__ constexpr int adc_qmax(int M) { return kAdcE8 ? 255 : 32767 / M; }
 
 __device__ __forceinline__ float wave_min(float v) {
 #pragma unroll
@@ -530,19 +556,22 @@ __global__ __launch_bounds__(256) void adc_qstats_kernel(const float* __restrict
     }
 }
 
-// grid (ceil(nq / QB), M), block 256 (code c): table block b = (M, 256, QB / 2) dwords, query
-// 2j in the low and 2j + 1 in the high half of dword j.  q <= (lut - min) / delta (the ratio
+// grid (ceil(nq / QB), M), block 256 (code c): table block b = (M, 256, NWD) dwords.  u16
+// entries: query 2j in the low and 2j + 1 in the high half of dword j.  u8 entries (E8): dword
+// w holds queries (4w, 4w + 2, 4w + 1, 4w + 3) in bytes 0..3, so the two byte-pair unpacks
+// give the u16 pairs (4w, 4w + 1) and (4w + 2, 4w + 3).  q <= (lut - min) / delta (the ratio
 // is shrunk by 2^-50 before the floor, so fp64 rounding never rounds it up past an integer).
 template <int QB>
 __global__ __launch_bounds__(256) void adc_qtab_kernel(const float* __restrict__ lut, int64_t nq, int M,
                                                        const float* __restrict__ mins,
                                                        const AdcQStat* __restrict__ qs, uint32_t* __restrict__ tab) {
+    constexpr int NWD = kAdcE8 ? QB / 4 : QB / 2;
     const int64_t qb = blockIdx.x;
     const int m = blockIdx.y, c = threadIdx.x;
     const int qmax = adc_qmax(M);
-    uint32_t w[QB / 2];
+    uint32_t w[NWD];
 #pragma unroll
-    for (int j = 0; j < QB / 2; ++j) w[j] = 0u;
+    for (int j = 0; j < NWD; ++j) w[j] = 0u;
 #pragma unroll
     for (int qq = 0; qq < QB; ++qq) {
         const int64_t qi = qb * QB + qq;
@@ -555,22 +584,50 @@ __global__ __launch_bounds__(256) void adc_qtab_kernel(const float* __restrict__
                 v = x >= (double)qmax ? (uint32_t)qmax : x > 0.0 ? (uint32_t)floor(x) : 0u;
             }
         }
-        w[qq >> 1] |= v << (16 * (qq & 1));
+        if constexpr (kAdcE8) {
+            const int r = qq & 3;
+            w[qq >> 2] |= v << (8 * (((r & 1) << 1) | (r >> 1)));
+        } else {
+            w[qq >> 1] |= v << (16 * (qq & 1));
+        }
     }
-    uint32_t* dst = tab + ((qb * M + m) * 256 + c) * (QB / 2);
+    uint32_t* dst = tab + ((qb * M + m) * 256 + c) * NWD;
+    if constexpr (NWD >= 4) {
 #pragma unroll
-    for (int j = 0; j < QB / 2; j += 4) *reinterpret_cast<uint4*>(dst + j) = make_uint4(w[j], w[j + 1], w[j + 2], w[j + 3]);
+        for (int j = 0; j < NWD; j += 4) *reinterpret_cast<uint4*>(dst + j) = make_uint4(w[j], w[j + 1], w[j + 2], w[j + 3]);
+    } else {
+        *reinterpret_cast<uint2*>(dst) = make_uint2(w[0], w[1]);
+    }
 }
 
-// grid (nchunks, ceil(nq / QB)), block kScanWaves waves (the fp32 scan's structure): the
-// integer tables of QB queries in LDS, M = 16 MC, each lane one row per wave-step with its
-// code row loaded a step ahead.  Part lists of (float(S), id), k per query.
-template <int R, int QB, int MC>
+// grid (nchunks, ceil(nq / 16)), block kScanWaves waves (the fp32 scan's structure): the u8
+// tables of 16 queries in LDS (M * 4 KiB), M = 16 MC, each lane one row per wave-step with its
+// code row loaded a step ahead.  No wave-level list during the scan: every lane keeps, per
+// query, the two smallest keys (S << 16 | wave-step) of its own rows (v_med3 + v_min per row
+// and query, registers only).  At the end each wave ("part") selects from its 128 lane
+// candidates per query those with S below T = the largest value with at most K1 candidates
+// below it (binary search on ballot counts), writes them (float(S), id) -- the rest of the K1
+// slots sentinels -- and its bound B = min(T, min over lanes of the lane's second key's S):
+// every row of the part that is not listed has S >= B (a lane's other rows are >= its second
+// key, a dropped candidate is >= T).  (The round-5 first cut kept wave-resident exact lists
+// updated by ballot + shuffle inserts: those inserts were most of its LDS instructions.)
+constexpr int kQB = 16;  // queries per integer-table block
+
+__device__ __forceinline__ uint32_t umed3(uint32_t a, uint32_t b, uint32_t c) {
+    uint32_t r;
+    asm("v_med3_u32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
+    return r;
+}
+
+template <int MC>
 __global__ __launch_bounds__(kScanWaves * 64) void adc_qscan_kernel(
-    const uint32_t* __restrict__ qtab, int64_t nq, const uint8_t* __restrict__ codes, int64_t n, int k,
-    int64_t id_offset, int64_t chunk_rows, float* __restrict__ part_d, uint32_t* __restrict__ part_i) {
+    const uint32_t* __restrict__ qtab, int64_t nq, const uint8_t* __restrict__ codes, int64_t n, int k1,
+    int64_t id_offset, int64_t chunk_rows, float* __restrict__ part_d, uint32_t* __restrict__ part_i,
+    float* __restrict__ part_b) {
     constexpr int M = 16 * MC;
-    constexpr int NWD = QB / 2;  // dwords per (m, code) entry
+    constexpr int QB = kQB;
+    constexpr int NWD = QB / 4;   // dwords per (m, code) entry (u8 per query)
+    constexpr int NACC = QB / 2;  // u16-pair accumulators (queries 2j, 2j + 1)
     extern __shared__ __attribute__((aligned(16))) uint32_t qt[];  // [M][256][NWD]
     const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
     const int64_t q0 = (int64_t)blockIdx.y * QB;
@@ -582,37 +639,27 @@ __global__ __launch_bounds__(kScanWaves * 64) void adc_qscan_kernel(
     }
     __syncthreads();
 
-    WaveTopK<R> top[QB];
-    float thr_d[QB];
-    uint32_t thr_i[QB];
+    uint32_t m1[QB], m2[QB];  // per query: the lane's two smallest (S << 16 | step), ~0u = none
 #pragma unroll
-    for (int qq = 0; qq < QB; ++qq) {
-        top[qq].init();
-        thr_d[qq] = INFINITY;
-        thr_i[qq] = kNoId;
-    }
-    // screen words: field j of query pair (2j, 2j+1) holds min(threshold, 0x7FFF) | 0x8000
-    uint32_t tw[NWD];
-#pragma unroll
-    for (int j = 0; j < NWD; ++j) tw[j] = 0xFFFFFFFFu;
+    for (int qq = 0; qq < QB; ++qq) m1[qq] = m2[qq] = 0xFFFFFFFFu;
 
     const int64_t rbeg = (int64_t)blockIdx.x * chunk_rows;
     const int64_t rend = min(n, rbeg + chunk_rows);
-    const uint32_t par = (uint32_t)lane & 1u;
-    const uint32_t tbase = (uint32_t)(uintptr_t)qt + (NWD == 8 ? 16u * par : 0u);
+    const uint32_t tbase = (uint32_t)(uintptr_t)qt;
     uint4 cw[MC];
     auto fetch = [&](int64_t row) __attribute__((always_inline)) {
         const uint4* cr = reinterpret_cast<const uint4*>(codes + row * (16 * MC));
 #pragma unroll
         for (int c = 0; c < MC; ++c) cw[c] = row < rend ? cr[c] : make_uint4(0u, 0u, 0u, 0u);
     };
-    fetch(rbeg + (int64_t)wv * 64 + lane);
-    for (int64_t base = rbeg + (int64_t)wv * 64; base < rend; base += kScanWaves * 64) {
+    const int64_t first = rbeg + (int64_t)wv * 64;
+    fetch(first + lane);
+    uint32_t step = 0;
+    for (int64_t base = first; base < rend; base += kScanWaves * 64, ++step) {
         const int64_t row = base + lane;
-        const bool valid = row < rend;
-        uint32_t acc[NWD];
+        uint32_t acc[NACC];
 #pragma unroll
-        for (int j = 0; j < NWD; ++j) acc[j] = 0u;
+        for (int j = 0; j < NACC; ++j) acc[j] = 0u;
         uint4 cur[MC];
 #pragma unroll
         for (int c = 0; c < MC; ++c) cur[c] = cw[c];
@@ -631,68 +678,67 @@ __global__ __launch_bounds__(kScanWaves * 64) void adc_qscan_kernel(
             for (int b = 0; b < 4; ++b) {
                 uint32_t cb, o1;
                 asm("v_bfe_u32 %0, %1, %2, 8" : "=v"(cb) : "v"(wrd), "i"(8 * b));
-                if constexpr (NWD == 8) {
-                    // 32-B entries as two 16-B halves, odd lanes in the opposite order (two 8-into-8
-                    // bank draws per 16-lane group, as the fp32 scan); integer sums do not care
-                    uint32_t o2;
-                    asm("v_lshl_add_u32 %0, %1, 5, %2" : "=v"(o1) : "v"(cb), "v"(wofs));
-                    asm("v_xor_b32 %0, 16, %1" : "=v"(o2) : "v"(o1));
-                    const u32x4v t0 = *(reinterpret_cast<const lds_u4*>((uintptr_t)o1) + b * 512);
-                    const u32x4v t1 = *(reinterpret_cast<const lds_u4*>((uintptr_t)o2) + b * 512);
-                    acc[0] += t0.x; acc[1] += t0.y; acc[2] += t0.z; acc[3] += t0.w;
-                    acc[4] += t1.x; acc[5] += t1.y; acc[6] += t1.z; acc[7] += t1.w;
-                } else {
-                    asm("v_lshl_add_u32 %0, %1, 4, %2" : "=v"(o1) : "v"(cb), "v"(wofs));
-                    const u32x4v t0 = *(reinterpret_cast<const lds_u4*>((uintptr_t)o1) + b * 256);
-                    acc[0] += t0.x; acc[1] += t0.y; acc[2] += t0.z; acc[3] += t0.w;
+                asm("v_lshl_add_u32 %0, %1, 4, %2" : "=v"(o1) : "v"(cb), "v"(wofs));
+                const u32x4v t0 = *(reinterpret_cast<const lds_u4*>((uintptr_t)o1) + b * 256);
+                const uint32_t tv[4] = {t0.x, t0.y, t0.z, t0.w};
+#pragma unroll
+                for (int wd = 0; wd < 4; ++wd) {  // bytes (4w, 4w+2, 4w+1, 4w+3) -> u16 pairs
+                    acc[2 * wd] += __builtin_amdgcn_perm(tv[wd], tv[wd], 0x0C020C00u);
+                    acc[2 * wd + 1] += __builtin_amdgcn_perm(tv[wd], tv[wd], 0x0C030C01u);
                 }
             }
 #pragma unroll
             for (int t = 0; t + 1 < 4 * MC; ++t) wq[t] = wq[t + 1];
         }
-        if constexpr (NWD == 8) {  // odd lanes hold the second half first
+        // a row past the chunk takes part in nothing (the last step only)
+        const uint32_t inval = row < rend ? 0u : 0xFFFFFFFFu;
 #pragma unroll
-            for (int j = 0; j < 4; ++j) {
-                const uint32_t a = acc[j], b2 = acc[j + 4];
-                acc[j] = par ? b2 : a;
-                acc[j + 4] = par ? a : b2;
-            }
-        }
-        uint32_t hit = 0u;
-#pragma unroll
-        for (int j = 0; j < NWD; ++j) hit |= (tw[j] - acc[j]) & 0x80008000u;
-        if (__ballot(valid && hit != 0u) == 0ull) continue;  // the common case: nothing to insert
-        const uint32_t gid = (uint32_t)(id_offset + row);
-#pragma unroll
-        for (int j = 0; j < NWD; ++j) {
-            // only the pairs whose screen fired (wave-uniform test)
-            if (__ballot(valid && ((tw[j] - acc[j]) & 0x80008000u) != 0u) == 0ull) continue;
-            uint32_t tnew = 0u;
-#pragma unroll
-            for (int h = 0; h < 2; ++h) {
-                const int qq = 2 * j + h;
-                if (qq < nqb) {
-                    const float key = (float)((acc[j] >> (16 * h)) & 0xFFFFu);
-                    top[qq].offer(valid, key, gid, k, lane, thr_d[qq], thr_i[qq]);
-                }
-                const uint32_t t = thr_d[qq] < 32767.0f ? (uint32_t)thr_d[qq] : 0x7FFFu;
-                tnew |= (t | 0x8000u) << (16 * h);
-            }
-            tw[j] = tnew;
+        for (int j = 0; j < NACC; ++j) {
+            const uint32_t klo = ((acc[j] << 16) | step) | inval;          // query 2j
+            const uint32_t khi = ((acc[j] & 0xFFFF0000u) | step) | inval;  // query 2j + 1
+            m2[2 * j] = umed3(m1[2 * j], m2[2 * j], klo);
+            m1[2 * j] = min(m1[2 * j], klo);
+            m2[2 * j + 1] = umed3(m1[2 * j + 1], m2[2 * j + 1], khi);
+            m1[2 * j + 1] = min(m1[2 * j + 1], khi);
         }
     }
+    // per query: select the candidates below T, the bound B, write K1 slots
     const int64_t part = (int64_t)blockIdx.x * kScanWaves + wv;
+    const uint64_t below = (1ull << lane) - 1ull;
 #pragma unroll
     for (int qq = 0; qq < QB; ++qq) {
-        if (qq < nqb) {
-            float* od = part_d + (part * nq + q0 + qq) * k;
-            uint32_t* oi = part_i + (part * nq + q0 + qq) * k;
-#pragma unroll
-            for (int r = 0; r < R; ++r) {
-                const int e = r * 64 + lane;
-                if (e < k) { od[e] = top[qq].d[r]; oi[e] = top[qq].id[r]; }
-            }
+        if (qq >= nqb) continue;
+        const uint32_t s1 = m1[qq] >> 16, s2 = m2[qq] >> 16;  // 0xFFFF: no candidate
+        // T: the largest t in [0, 0xFFFF] with #{candidates with S < t} <= k1
+        uint32_t lo = 0, hi = 0xFFFF;  // keys of rows past the chunk have S = 0xFFFF: never candidates
+        while (lo < hi) {  // wave-uniform
+            const uint32_t mid = (lo + hi + 1) >> 1;
+            const int cnt = __popcll(__ballot(s1 < mid)) + __popcll(__ballot(s2 < mid));
+            if (cnt <= k1) lo = mid; else hi = mid - 1;
         }
+        const uint32_t T = lo;
+        // min over lanes of the second key's S (ballot binary search: the largest t with no s2 < t)
+        uint32_t blo = 0, bhi = 0xFFFF;
+        while (blo < bhi) {
+            const uint32_t mid = (blo + bhi + 1) >> 1;
+            if (__ballot(s2 < mid) == 0ull) blo = mid; else bhi = mid - 1;
+        }
+        const uint32_t B = min(T, blo);
+        float* od = part_d + (part * nq + q0 + qq) * k1;
+        uint32_t* oi = part_i + (part * nq + q0 + qq) * k1;
+        const bool t1 = s1 < T, t2 = s2 < T;
+        const uint64_t b1 = __ballot(t1), b2 = __ballot(t2);
+        const int n1 = __popcll(b1);
+        const int p1 = __popcll(b1 & below), p2 = n1 + __popcll(b2 & below);
+        auto rid = [&](uint32_t key) {
+            return (uint32_t)(id_offset + first + (int64_t)(key & 0xFFFFu) * (kScanWaves * 64) + lane);
+        };
+        if (t1) { od[p1] = (float)s1; oi[p1] = rid(m1[qq]); }
+        if (t2) { od[p2] = (float)s2; oi[p2] = rid(m2[qq]); }
+        const int used = n1 + __popcll(b2);
+        for (int e = used + lane; e < k1; e += 64) { od[e] = INFINITY; oi[e] = kNoId; }
+        // B = 0xFFFF: every row of the part is listed
+        if (lane == 0) part_b[part * nq + q0 + qq] = B >= 0xFFFFu ? INFINITY : (float)B;
     }
 }
 
@@ -700,8 +746,8 @@ __global__ __launch_bounds__(kScanWaves * 64) void adc_qscan_kernel(
 template <int R, int MC>
 __global__ __launch_bounds__(256) void adc_rerank_kernel(const float* __restrict__ lut, int64_t nq,
                                                          const uint8_t* __restrict__ codes, int64_t id_offset,
-                                                         const float* __restrict__ pd, const uint32_t* __restrict__ pi,
-                                                         int parts, int k, const AdcQStat* __restrict__ qs,
+                                                         const uint32_t* __restrict__ pi, const float* __restrict__ pb,
+                                                         int parts, int k1, int k, const AdcQStat* __restrict__ qs,
                                                          float* __restrict__ out_d, uint32_t* __restrict__ out_i,
                                                          int* __restrict__ fail_list, int* __restrict__ fail_count) {
     constexpr int M = 16 * MC;
@@ -714,13 +760,13 @@ __global__ __launch_bounds__(256) void adc_rerank_kernel(const float* __restrict
     float thr_d = INFINITY;
     uint32_t thr_i = kNoId;
     const float* lq = lut + qi * M * 256;
-    const int64_t total = (int64_t)parts * k;
+    const int64_t total = (int64_t)parts * k1;
     for (int64_t e0 = 0; e0 < total; e0 += 64) {
         const int64_t e = e0 + lane;
         uint32_t id = kNoId;
         if (e < total) {
-            const int64_t p = e / k, j = e - p * k;
-            id = pi[(p * nq + qi) * k + j];
+            const int64_t p = e / k1, j = e - p * k1;
+            id = pi[(p * nq + qi) * k1 + j];
         }
         const bool valid = id != kNoId;
         float dv = INFINITY;
@@ -744,15 +790,15 @@ __global__ __launch_bounds__(256) void adc_rerank_kernel(const float* __restrict
         }
         top.offer(valid, dv, id, k, lane, thr_d, thr_i);
     }
-    // certificate: every full part list's k-th S must bound its missing rows above E_k
+    // certificate: every part's bound B (its unlisted rows have S >= B) must put them above E_k
     bool ok = !st.bad;
     for (int p0 = 0; p0 < parts; p0 += 64) {
         const int p = p0 + lane;
         bool f = false;
         if (p < parts) {
-            const int64_t at = ((int64_t)p * nq + qi) * k + (k - 1);
-            if (pi[at] != kNoId) {
-                const double lb = st.base + st.delta * (double)pd[at] - st.margin;
+            const float B = pb[(int64_t)p * nq + qi];
+            if (B < INFINITY) {
+                const double lb = st.base + st.delta * (double)B - st.margin;
                 f = !(lb > (double)thr_d);
             }
         }
@@ -809,10 +855,17 @@ hipError_t launch_scan(const float* lut, int64_t nq, const uint8_t* codes, int64
     hipError_t e = hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);
     if (e != hipSuccess) return e;
     const int64_t chunk_rows = ceil_div(n, nch);
-    hipLaunchKernelGGL(kern, dim3((unsigned)nch, (unsigned)ceil_div(nq, QB)), dim3(kScanWaves * 64), smem, st, lut, nq, codes,
+    // the re-run of uncertified queries: one round of workgroups looping over the list slots
+    const int64_t qgrid = qlist != nullptr ? std::max<int64_t>(1, std::min<int64_t>(ceil_div(nq, QB), 256 / nch))
+                                           : ceil_div(nq, QB);
+    hipLaunchKernelGGL(kern, dim3((unsigned)nch, (unsigned)qgrid), dim3(kScanWaves * 64), smem, st, lut, nq, codes,
                        n, M, ksub, k, id_offset, chunk_rows, pd, pi, qlist, qcount);
     return hipGetLastError();
 }
+
+// Row chunks of the re-run of uncertified queries: ~32k rows each (one failed query costs a
+// few tens of microseconds, not a whole-database workgroup).
+int64_t adc_fallback_chunks(int64_t n) { return std::max<int64_t>(1, std::min<int64_t>(256, ceil_div(n, 32768))); }
 
 template <int R>
 hipError_t launch_scan_r(int QB, const float* lut, int64_t nq, const uint8_t* codes, int64_t n, int M, int ksub,
@@ -861,71 +914,88 @@ hipError_t launch_flat_r(int QB, const float* q, int64_t nq, const float* x, int
 // Filtered path eligibility by shape (the workspace is sized on shape alone) and the profiling
 // switch MIVQ_ADC_EXACT=1 (the fp32 scan for every query).
 // (queries per table block: the variants whose lists fit the 128 registers of the 16-wave scan)
-bool adc_filtered_shape(int M, int ksub, int k) {
-    return ksub == 256 && (M == 16 || (M == 32 && k <= 192)) && k <= 256;
-}
-int adc_fqb(int M, int k) { return M == 16 && k <= 64 ? 16 : 8; }
+// Part lists keep K1 = k + kListSlack entries (at most 256): the certificate bounds the rows a
+// part did NOT list by its K1-th entry, so a part holding some of the k best rows still
+// certifies when its K1-th row is clearly worse (with K1 = k, the part holding the best row of
+// a k = 1 search never could).
+constexpr int kListSlack = 4;
+int adc_k1(int k) { return k + kListSlack; }
+// k <= 32: a part's 128 lane candidates (two per lane) carry the k best rows with room to spare;
+// for larger k the per-lane bound (a lane's second-best) sits too close to the k-th distance to
+// certify, and the fp32 scan serves those searches
+bool adc_filtered_shape(int M, int ksub, int k) { return ksub == 256 && (M == 16 || M == 32) && k <= 32; }
+int adc_fqb(int M, int k) { return kQB; }
 
 struct AdcFilteredLayout {
-    size_t stats, mins, tab, p1d, p1i, fail, total;
+    size_t stats, mins, tab, p1d, p1i, p1b, fail, total;
     int64_t nch, parts;
+    int k1;
 };
 
 AdcFilteredLayout adc_filtered_layout(int64_t nq, int64_t n, int M, int k, size_t off) {
     AdcFilteredLayout L{};
     const int QB = adc_fqb(M, k);
-    L.nch = adc_chunks(nq, n, QB);
+    L.k1 = adc_k1(k);
+    // a lane's step index is 16 bits: at most 65535 wave-steps (of 1024 rows) per chunk
+    L.nch = std::max<int64_t>(adc_chunks(nq, n, QB), ceil_div(n, (int64_t)65535 * kScanWaves * 64));
     L.parts = L.nch * kScanWaves;
     L.stats = off;  off = align_up(off + (size_t)nq * sizeof(AdcQStat), 256);
     L.mins = off;   off = align_up(off + (size_t)nq * M * sizeof(float), 256);
-    L.tab = off;    off = align_up(off + (size_t)ceil_div(nq, QB) * M * 256 * (QB / 2) * sizeof(uint32_t), 256);
-    L.p1d = off;    off = align_up(off + (size_t)L.parts * nq * k * sizeof(float), 256);
-    L.p1i = off;    off = align_up(off + (size_t)L.parts * nq * k * sizeof(uint32_t), 256);
+    L.tab = off;    off = align_up(off + (size_t)ceil_div(nq, QB) * M * 256 * QB * (kAdcE8 ? 1 : 2), 256);
+    L.p1d = off;    off = align_up(off + (size_t)L.parts * nq * L.k1 * sizeof(float), 256);
+    L.p1i = off;    off = align_up(off + (size_t)L.parts * nq * L.k1 * sizeof(uint32_t), 256);
+    L.p1b = off;    off = align_up(off + (size_t)L.parts * nq * sizeof(float), 256);
     L.fail = off;   off = align_up(off + (size_t)(nq + 1) * sizeof(int), 256);
     L.total = off;
     return L;
 }
 
-template <int R, int MC, int QB>
-hipError_t launch_filtered_r(const float* lut, int64_t nq, const uint8_t* codes, int64_t n, int k, int64_t id_offset,
-                             unsigned char* ws, const AdcFilteredLayout& L, float* dists, uint32_t* ids,
-                             hipStream_t st) {
+template <int MC>
+hipError_t launch_qscan(const uint32_t* tab, int64_t nq, const uint8_t* codes, int64_t n, int k1, int64_t id_offset,
+                        const AdcFilteredLayout& L, float* p1d, uint32_t* p1i, float* p1b, hipStream_t st) {
     constexpr int M = 16 * MC;
-    auto* qs = reinterpret_cast<AdcQStat*>(ws + L.stats);
-    auto* mins = reinterpret_cast<float*>(ws + L.mins);
-    auto* tab = reinterpret_cast<uint32_t*>(ws + L.tab);
-    auto* p1d = reinterpret_cast<float*>(ws + L.p1d);
-    auto* p1i = reinterpret_cast<uint32_t*>(ws + L.p1i);
-    int* fail_count = reinterpret_cast<int*>(ws + L.fail);
-    int* fail_list = fail_count + 1;
-    hipError_t e = hipMemsetAsync(fail_count, 0, sizeof(int), st);
+    auto kern = adc_qscan_kernel<MC>;
+    const int smem = M * 256 * kQB;
+    const hipError_t e = hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, smem);
     if (e != hipSuccess) return e;
-    hipLaunchKernelGGL(adc_qstats_kernel, dim3((unsigned)nq), dim3(256), 0, st, lut, nq, M, mins, qs);
-    const int64_t qblocks = ceil_div(nq, QB);
-    hipLaunchKernelGGL(adc_qtab_kernel<QB>, dim3((unsigned)qblocks, (unsigned)M), dim3(256), 0, st, lut, nq, M, mins, qs,
-                       tab);
-    auto kern = adc_qscan_kernel<R, QB, MC>;
-    const int smem = M * 256 * QB * 2;
-    e = hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, smem);
-    if (e != hipSuccess) return e;
-    hipLaunchKernelGGL(kern, dim3((unsigned)L.nch, (unsigned)qblocks), dim3(kScanWaves * 64), smem, st, tab, nq, codes, n,
-                       k, id_offset, ceil_div(n, L.nch), p1d, p1i);
-    hipLaunchKernelGGL((adc_rerank_kernel<R, MC>), dim3((unsigned)ceil_div(nq, 4)), dim3(256), 0, st, lut, nq, codes,
-                       id_offset, p1d, p1i, (int)L.parts, k, qs, dists, ids, fail_list, fail_count);
+    hipLaunchKernelGGL(kern, dim3((unsigned)L.nch, (unsigned)ceil_div(nq, kQB)), dim3(kScanWaves * 64), smem, st, tab,
+                       nq, codes, n, k1, id_offset, ceil_div(n, L.nch), p1d, p1i, p1b);
     return hipGetLastError();
 }
 
 hipError_t launch_filtered(int M, const float* lut, int64_t nq, const uint8_t* codes, int64_t n, int k,
                            int64_t id_offset, unsigned char* ws, const AdcFilteredLayout& L, float* dists,
                            uint32_t* ids, hipStream_t st) {
+    const int QB = adc_fqb(M, k), k1 = L.k1;
+    auto* qs = reinterpret_cast<AdcQStat*>(ws + L.stats);
+    auto* mins = reinterpret_cast<float*>(ws + L.mins);
+    auto* tab = reinterpret_cast<uint32_t*>(ws + L.tab);
+    auto* p1d = reinterpret_cast<float*>(ws + L.p1d);
+    auto* p1i = reinterpret_cast<uint32_t*>(ws + L.p1i);
+    auto* p1b = reinterpret_cast<float*>(ws + L.p1b);
+    int* fail_count = reinterpret_cast<int*>(ws + L.fail);
+    int* fail_list = fail_count + 1;
+    hipError_t e = hipMemsetAsync(fail_count, 0, sizeof(int), st);
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(adc_qstats_kernel, dim3((unsigned)nq), dim3(256), 0, st, lut, nq, M, mins, qs);
+    const dim3 tgrid((unsigned)ceil_div(nq, QB), (unsigned)M);
+    if (QB == 16)
+        hipLaunchKernelGGL(adc_qtab_kernel<16>, tgrid, dim3(256), 0, st, lut, nq, M, mins, qs, tab);
+    else
+        hipLaunchKernelGGL(adc_qtab_kernel<8>, tgrid, dim3(256), 0, st, lut, nq, M, mins, qs, tab);
+    e = M == 16 ? launch_qscan<1>(tab, nq, codes, n, k1, id_offset, L, p1d, p1i, p1b, st)
+                : launch_qscan<2>(tab, nq, codes, n, k1, id_offset, L, p1d, p1i, p1b, st);
+    if (e != hipSuccess) return e;
     const int R = (k + 63) / 64;
-#define MIVQ_F(RR, MCC, QBB) \
-    return launch_filtered_r<RR, MCC, QBB>(lut, nq, codes, n, k, id_offset, ws, L, dists, ids, st)
-    if (M == 16) {
-        switch (R) { case 1: MIVQ_F(1, 1, 16); case 2: MIVQ_F(2, 1, 8); case 3: MIVQ_F(3, 1, 8); default: MIVQ_F(4, 1, 8); }
-    }
-    switch (R) { case 1: MIVQ_F(1, 2, 8); case 2: MIVQ_F(2, 2, 8); default: MIVQ_F(3, 2, 8); }
-#undef MIVQ_F
+    const dim3 rgrid((unsigned)ceil_div(nq, 4));
+#define MIVQ_RR(RR, MM)                                                                                              \
+    hipLaunchKernelGGL((adc_rerank_kernel<RR, MM>), rgrid, dim3(256), 0, st, lut, nq, codes, id_offset, p1i, p1b, \
+                       (int)L.parts, k1, k, qs, dists, ids, fail_list, fail_count)
+    (void)R;  // k <= 32: one list register
+    if (M == 16) MIVQ_RR(1, 1);
+    else MIVQ_RR(1, 2);
+#undef MIVQ_RR
+    return hipGetLastError();
 }
 
 }  // namespace
@@ -1026,7 +1096,8 @@ extern "C" size_t mivq_adc_search_workspace_bytes(int64_t nq, int64_t n, int32_t
     if (nq <= 0 || n <= 0 || M <= 0 || k <= 0 || nbits < 1 || nbits > 8) return 0;
     const int QB = adc_qb(M, 1 << nbits);
     if (QB == 0) return 0;
-    const int64_t parts = adc_chunks(nq, n, QB) * kScanWaves;
+    int64_t parts = adc_chunks(nq, n, QB) * kScanWaves;
+    if (adc_filtered_shape(M, 1 << nbits, k)) parts = std::max<int64_t>(parts, adc_fallback_chunks(n) * kScanWaves);
     // the fp32 scan's part lists (every query, or the filtered path's uncertified ones) ...
     const size_t exact = align_up((size_t)parts * nq * k * sizeof(float), 256) + align_up((size_t)parts * nq * k * 4, 256);
     // ... then the filtered path's regions
@@ -1059,30 +1130,39 @@ extern "C" int mivq_adc_search(const float* lut, int64_t nq, const uint8_t* code
     const size_t need = mivq_adc_search_workspace_bytes(nq, n, M, nbits, k);
     MIVQ_REQUIRE(workspace && workspace_bytes >= need, MIVQ_ERR_WORKSPACE, "adc_search: workspace %zu < %zu",
                  workspace_bytes, need);
-    const int64_t nch = adc_chunks(nq, n, QB);
-    const int parts = (int)(nch * kScanWaves);
+    const bool fshape = adc_filtered_shape(M, ksub, k);
+    const int64_t nch_exact = adc_chunks(nq, n, QB), nch_fb = adc_fallback_chunks(n);
+    const int64_t parts_ws = std::max<int64_t>(nch_exact, fshape ? nch_fb : 0) * kScanWaves;
     float* pd = static_cast<float*>(workspace);
-    const size_t exact_bytes = align_up((size_t)parts * nq * k * sizeof(float), 256) + align_up((size_t)parts * nq * k * 4, 256);
+    const size_t exact_bytes = align_up((size_t)parts_ws * nq * k * sizeof(float), 256) +
+                               align_up((size_t)parts_ws * nq * k * 4, 256);
     uint32_t* pi = reinterpret_cast<uint32_t*>(static_cast<unsigned char*>(workspace) +
-                                               align_up((size_t)parts * nq * k * sizeof(float), 256));
+                                               align_up((size_t)parts_ws * nq * k * sizeof(float), 256));
     // the filtered path (integer-LUT scan + exact re-rank + certificate; the fp32 scan re-runs
     // only the uncertified queries): same results, ~half the LDS traffic per (query, row)
     const char* force_exact = getenv("MIVQ_ADC_EXACT");  // profiling: the fp32 scan for every query
-    const bool filtered = adc_filtered_shape(M, ksub, k) && reinterpret_cast<uintptr_t>(codes) % 16 == 0 &&
+    const bool filtered = fshape && reinterpret_cast<uintptr_t>(codes) % 16 == 0 &&
                           reinterpret_cast<uintptr_t>(lut) % 16 == 0 && !(force_exact && atoi(force_exact) != 0);
     const int* qlist = nullptr;
     const int* qcount = nullptr;
     hipError_t e;
+    const char* nofb = getenv("MIVQ_ADC_NO_FALLBACK");  // tests: certified queries only, the others NaN
+    const bool no_fallback = nofb && atoi(nofb) != 0;
     if (filtered) {
         const AdcFilteredLayout FL = adc_filtered_layout(nq, n, M, k, exact_bytes);
         unsigned char* ws = static_cast<unsigned char*>(workspace);
+        if (no_fallback) {
+            e = hipMemsetAsync(dists, 0xFF, (size_t)nq * k * sizeof(float), st);
+            if (e != hipSuccess) return set_error(MIVQ_ERR_HIP, "adc_search: %s", hipGetErrorString(e));
+        }
         e = launch_filtered(M, lut, nq, codes, n, k, id_offset, ws, FL, dists, ids, st);
         if (e != hipSuccess) return set_error(MIVQ_ERR_HIP, "adc_search (filtered): %s", hipGetErrorString(e));
         qcount = reinterpret_cast<const int*>(ws + FL.fail);
         qlist = qcount + 1;
-        const char* nofb = getenv("MIVQ_ADC_NO_FALLBACK");  // tests: certified queries only (others unset)
-        if (nofb && atoi(nofb) != 0) return MIVQ_OK;
+        if (no_fallback) return MIVQ_OK;
     }
+    const int64_t nch = filtered ? nch_fb : nch_exact;
+    const int parts = (int)(nch * kScanWaves);
     const int R = (k + 63) / 64;
     switch (R) {
         case 1: e = launch_scan_r<1>(QB, lut, nq, codes, n, M, ksub, k, id_offset, nch, pd, pi, st, qlist, qcount); break;

@@ -61,6 +61,19 @@ constexpr int kWideWaves = 4;
 constexpr int cs_waves(int KS) { return KS <= 6 ? kWaves : kWideWaves; }
 constexpr int kRsrcWord3 = 0x00020000;  // gfx9 buffer resource: 32-bit data format
 constexpr int kXAux = 2;  // x stream cache policy: nt (read once; round 4 measured the others)
+#ifndef MIVQ_AB_XAUX48  // A/B builds (tools/build_ab.sh): the dsub-48 filter's policy
+#define MIVQ_AB_XAUX48 2
+#endif
+constexpr int kXAux48 = MIVQ_AB_XAUX48;
+#ifndef MIVQ_AB_DIRECT  // A/B builds: 1 = codes stored in the (n, M) output layout directly (no transpose launch)
+#define MIVQ_AB_DIRECT 0
+#endif
+constexpr bool kDirect = MIVQ_AB_DIRECT != 0;
+// Byte of (row, subspace m) in the code buffer: (M, n) scratch (then transposed), or the (n, M)
+// output itself (kDirect).
+__device__ __forceinline__ int64_t code_at(int64_t row, int m, int64_t n, int M) {
+    return kDirect ? row * M + m : (int64_t)m * n + row;
+}
 
 // Keeps the three largest of a stream of packed scores.  Inline asm because the compiler
 // quiets every packed value (v_max_f32 v, v, v) before fmaxf / fmed3 in IEEE mode: the
@@ -303,7 +316,7 @@ __global__ __launch_bounds__(NW * 64) void pq_encode_cs_kernel(
                 // the block's uniform offset goes in soffset (SALU; gfx950 range-checks
                 // voffset + soffset, tools/probes/soffset_range.hip), the lane's in voffset
                 const int so = (vb * 32 + ibase(i)) * XS * 4 + hh * (16 * KT * 4);
-                const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(xr_rsrc, voff[i % PER], so, kXAux);
+                const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(xr_rsrc, voff[i % PER], so, DS == 48 ? kXAux48 : kXAux);
                 dst[i] = make_float4(__uint_as_float(v[0]), __uint_as_float(v[1]), __uint_as_float(v[2]),
                                      __uint_as_float(v[3]));
             }
@@ -348,7 +361,7 @@ __global__ __launch_bounds__(NW * 64) void pq_encode_cs_kernel(
         const float w12 = 1.0625f * (fmaf(4.8828125e-4f, pend_xs, b2.z) * pend_pd.x + pend_xs * pend_pd.y +
                                      b2.x * pend_xs + b2.y);
         if (pend_gap > w12) {
-            codesT[(int64_t)m * n + r0 + pend_row] = (uint8_t)(pend_k & 0xFF);
+            codesT[code_at(r0 + pend_row, m, n, M)] = (uint8_t)(pend_k & 0xFF);
             return false;
         }
         return true;
@@ -529,7 +542,7 @@ __global__ __launch_bounds__(NW * 64) void pq_encode_cs_kernel(
         const int k2 = (int)(__float_as_uint(t2) & 0xFFu);
         const int rowl = vb * 32 + r;
         const bool mine = (h == 0) && rowl < nrows;
-        if (mine && ncand == 1) codesT[(int64_t)m * n + r0 + rowl] = (uint8_t)k1;
+        if (mine && ncand == 1) codesT[code_at(r0 + rowl, m, n, M)] = (uint8_t)k1;
         const float gap = __fmul_rn(__fsub_rn(t1, t2), 0.99999988f);  // rounded down
         if (kR3Loop && pdw != nullptr) {
             // round-3 tail (dsub 64, generic shapes): settle the previous block's pair, then
@@ -950,7 +963,7 @@ __global__ __launch_bounds__(kMWaves * 64) __attribute__((amdgpu_waves_per_eu(1,
                 if (h == 0 && r < cntb) {
                     const unsigned long long key = gkeys[r];
                     // (s, k) minimum; no finite-or--inf candidate (all NaN / +inf) -> 0, as below
-                    codesT[(int64_t)m * n + r0 + rowl] = (uint8_t)((uint32_t)(key >> 32) < 0xFF800000u ? (key & 0xFF) : 0);
+                    codesT[code_at(r0 + rowl, m, n, M)] = (uint8_t)((uint32_t)(key >> 32) < 0xFF800000u ? (key & 0xFF) : 0);
                 }
                 return;
             }
@@ -982,7 +995,7 @@ __global__ __launch_bounds__(kMWaves * 64) __attribute__((amdgpu_waves_per_eu(1,
         const float os = __shfl_xor(bs, 32);
         const int ok = __shfl_xor(bk, 32);
         if (os < bs || (os == bs && ok < bk)) { bs = os; bk = ok; }
-        if (h == 0 && r < cntb) codesT[(int64_t)m * n + r0 + rowl] = (uint8_t)((bs < INFINITY) ? bk : 0);
+        if (h == 0 && r < cntb) codesT[code_at(r0 + rowl, m, n, M)] = (uint8_t)((bs < INFINITY) ? bk : 0);
     };
     // pair batch (rows staged): lane (r, 0) runs the chain of k1, lane (r, 1) that of k2
     auto pair_batch = [&](int cntb, uint2 it) __attribute__((always_inline)) {
@@ -1008,13 +1021,17 @@ __global__ __launch_bounds__(kMWaves * 64) __attribute__((amdgpu_waves_per_eu(1,
         if (h == 0 && r < cntb) {
             // (s1, k1) here, (s2, k2) from the partner: smallest (s, k), NaN never wins
             const bool two = os < sc || (os == sc && k2 < k1) || (sc != sc && os == os);
-            codesT[(int64_t)m * n + r0 + rowl] = (uint8_t)(two ? k2 : k1);
+            codesT[code_at(r0 + rowl, m, n, M)] = (uint8_t)(two ? k2 : k1);
         }
     };
 
     // Full batches first (claimed from ctr[0]; their A operands take 192 registers, so their
     // gathers are not prefetched), then pair batches (claimed from ctr[1]) with the next pair
     // batch's gather in flight while the current one is computed.
+#ifndef MIVQ_AB_RES  // A/B builds: 1 = the A operands loaded once per wave, 2 = and the next full batch's gather in flight
+#define MIVQ_AB_RES 0
+#endif
+    if constexpr (MIVQ_AB_RES == 0 || GC) {
     for (;;) {
             int b = 0;
             if (l == 0) b = atomicAdd(&ctr[0], 1);
@@ -1036,6 +1053,58 @@ __global__ __launch_bounds__(kMWaves * 64) __attribute__((amdgpu_waves_per_eu(1,
             full_batch(aa, cntb, (int)it.x);
             lds_fence();  // the tile is rewritten by the next commit
         }
+    } else if (nbf > 0) {
+        half8 aa[8][KS];
+#pragma unroll
+        for (int cb = 0; cb < 8; ++cb)
+#pragma unroll
+            for (int ks = 0; ks < KS; ++ks) aa[cb][ks] = im[(cb * KS + ks) * 64 + l];
+        auto claim_full = [&]() __attribute__((always_inline)) {
+            int bb = 0;
+            if (l == 0) bb = atomicAdd(&ctr[0], 1);
+            return __builtin_amdgcn_readfirstlane(__shfl(bb, 0));
+        };
+        if constexpr (MIVQ_AB_RES == 1) {
+            for (;;) {
+                const int b = claim_full();
+                if (b >= nbf) break;
+                uint2 it;
+                int cntb;
+                batch_info(b, it, cntb);
+                f32x4 v[NL];
+                gather_issue(cntb, (int)it.x, v);
+                gather_commit(v);
+                full_batch(aa, cntb, (int)it.x);
+                lds_fence();
+            }
+        } else {
+            int fb = claim_full();
+            uint2 fit = make_uint2(0u, 0u);
+            int fcnt = 0;
+            f32x4 fa[NL], fb2[NL];
+            if (fb < nbf) batch_info(fb, fit, fcnt);
+            gather_issue(fb < nbf ? fcnt : 0, (int)fit.x, fa);
+            auto fiter = [&](const f32x4 (&vc)[NL], f32x4 (&vn)[NL]) __attribute__((always_inline)) {
+                const int bn = claim_full();
+                uint2 itn = make_uint2(0u, 0u);
+                int cntn = 0;
+                if (bn < nbf) batch_info(bn, itn, cntn);
+                __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
+                gather_commit(vc);
+                gather_issue(cntn, (int)itn.x, vn);
+                full_batch(aa, fcnt, (int)fit.x);
+                lds_fence();
+                fb = bn;
+                fit = itn;
+                fcnt = cntn;
+            };
+            while (fb < nbf) {
+                fiter(fa, fb2);
+                if (fb >= nbf) break;
+                fiter(fb2, fa);
+            }
+        }
+    }
     // pair batches: the first one per wave is static (b = w), the rest are claimed from ctr[1]
     int b = w, cntb = 0;
     uint2 it = make_uint2(0u, 0u);
@@ -1246,7 +1315,8 @@ hipError_t launch_pq_encode_cs(int KS, const float* x, int64_t n, int d, int M, 
     switch (KS) {
 #define MIVQ_CS_CASE(k)                                                                                        \
     case k:                                                                                                    \
-        e = launch_pq_encode_cs_v<k>(x, n, d, M, dsub, C, cn, img, hinit, bnd, pd, bnd2, codesT, items, counts, st); \
+        e = launch_pq_encode_cs_v<k>(x, n, d, M, dsub, C, cn, img, hinit, bnd, pd, bnd2, kDirect ? codes : codesT, \
+                                     items, counts, st);                                                       \
         break;
         MIVQ_CS_CASE(1) MIVQ_CS_CASE(2) MIVQ_CS_CASE(3) MIVQ_CS_CASE(4) MIVQ_CS_CASE(5) MIVQ_CS_CASE(6)
         MIVQ_CS_CASE(7) MIVQ_CS_CASE(8) MIVQ_CS_CASE(9) MIVQ_CS_CASE(10) MIVQ_CS_CASE(11) MIVQ_CS_CASE(12)
@@ -1254,6 +1324,7 @@ hipError_t launch_pq_encode_cs(int KS, const float* x, int64_t n, int d, int M, 
         default: return hipErrorInvalidValue;
     }
     if (e != hipSuccess) return e;
+    if (kDirect) return hipSuccess;  // the kernels wrote the (n, M) layout
     const bool v16 = n % 16 == 0 && (reinterpret_cast<uintptr_t>(codesT) % 16) == 0 &&
                      (reinterpret_cast<uintptr_t>(codes) % 16) == 0 && M <= 256;
     if (v16 && M == 16)

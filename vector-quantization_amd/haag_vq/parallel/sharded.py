@@ -23,6 +23,7 @@ Callers: ``bench.py --gpus N`` (BASELINE config #5), ``vq-benchmark streaming-sw
 
 from __future__ import annotations
 
+from pathlib import Path
 from typing import Callable, Literal, Optional, Tuple
 
 import numpy as np
@@ -197,6 +198,35 @@ class ShardedFlatIndex(BaseSearchIndex):
 
     def memory_footprint(self) -> int:
         return int(self._codes.numel() * self._codes.element_size()) if self._codes is not None else 0
+
+    # --------------------------------------------------------------- persistence
+    @staticmethod
+    def shard_path(path, rank: int, world: int) -> Path:
+        """Each rank's file: <path>.rank<r>of<G>.npz (plain arrays, allow_pickle=False)."""
+        return Path(f"{path}.rank{rank}of{world}.npz")
+
+    def save(self, path) -> None:
+        from ..methods.search.flat_quantized_index import quantizer_state
+
+        rank, world = _world()
+        f = self.shard_path(path, rank, world)
+        f.parent.mkdir(parents=True, exist_ok=True)
+        st = {"codes": _arrays.to_host(self._codes), "metric": np.array(self._metric), "N": np.array(self._N),
+              "n_local": np.array(self._n_local), "offset": np.array(self._offset), "D": np.array(self._D)}
+        st.update(quantizer_state(self._quantizer))
+        with open(f, "wb") as fh:
+            np.savez(fh, **st)
+
+    def load(self, path) -> None:
+        from ..methods.search.flat_quantized_index import quantizer_from_state
+
+        rank, world = _world()
+        with np.load(self.shard_path(path, rank, world), allow_pickle=False) as z:
+            self._quantizer = quantizer_from_state(z)
+            self._codes = torch.from_numpy(np.array(z["codes"])).to(_arrays.device())
+            self._metric = str(z["metric"])
+            self._N, self._n_local = int(z["N"]), int(z["n_local"])
+            self._offset, self._D = int(z["offset"]), int(z["D"])
 
     def reconstruction_mse(self, X, sample_ids: Optional[np.ndarray] = None) -> Optional[float]:
         """Per-element MSE of this rank's rows (X: the local shard)."""

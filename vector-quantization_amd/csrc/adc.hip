@@ -498,11 +498,28 @@ struct AdcQStat {
 // Table entries: u16 per query (QMAX = 32767 / M), or u8 (QMAX = 255, E8: half the table
 // bytes again; unpacked to the u16 fields by two v_perm_b32 per dword).
 constexpr bool kAdcE8 = true;  // u8 entries (round 5: the u16 table measured no faster per call)
-__host__ __device__ constexpr int adc_qmax(int M) { return kAdcE8 ? 255 : 32767 / M; }
+#ifndef MIVQ_AB_ADC_SPAN  // A/B builds: the integer grid's span in mean offsets
+#define MIVQ_AB_ADC_SPAN 2.0
+#endif
+constexpr double kAdcSpan = MIVQ_AB_ADC_SPAN;
+#ifndef MIVQ_AB_ADC_BITS  // A/B builds: bits per integer-table entry (8, 7 or 6)
+#define MIVQ_AB_ADC_BITS 6
+#endif
+#ifndef MIVQ_AB_ADC_KEYS  // A/B builds: keys kept per lane and query (2 or 3)
+#define MIVQ_AB_ADC_KEYS 3
+#endif
+constexpr int kAdcBits = MIVQ_AB_ADC_BITS;
+constexpr int kLaneKeys = MIVQ_AB_ADC_KEYS;
+__host__ __device__ constexpr int adc_qmax(int M) { return kAdcE8 ? (1 << kAdcBits) - 1 : 32767 / M; }
 
 __device__ __forceinline__ float wave_min(float v) {
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) v = fminf(v, __shfl_xor(v, o));
+    return v;
+}
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
     return v;
 }
 __device__ __forceinline__ float wave_max(float v) {
@@ -515,7 +532,7 @@ __device__ __forceinline__ float wave_max(float v) {
 // query's {base, delta, margin, bad}.
 __global__ __launch_bounds__(256) void adc_qstats_kernel(const float* __restrict__ lut, int64_t nq, int M,
                                                          float* __restrict__ mins, AdcQStat* __restrict__ qs) {
-    __shared__ double s_min[64], s_rng[64], s_abs[64];
+    __shared__ double s_min[64], s_rng[64], s_abs[64], s_wid[64];
     __shared__ int s_bad;
     const int64_t qi = blockIdx.x;
     const int w = threadIdx.x >> 6, l = threadIdx.x & 63;
@@ -527,9 +544,12 @@ __global__ __launch_bounds__(256) void adc_qstats_kernel(const float* __restrict
         const float mn = wave_min(fminf(fminf(v.x, v.y), fminf(v.z, v.w)));
         const float mx = wave_max(fmaxf(fmaxf(v.x, v.y), fmaxf(v.z, v.w)));
         const float ab = wave_max(fmaxf(fmaxf(fabsf(v.x), fabsf(v.y)), fmaxf(fabsf(v.z), fabsf(v.w))));
+        // mean offset above the minimum (the scale the rows near the top live on)
+        const float wid = wave_sum((v.x - mn) + (v.y - mn) + (v.z - mn) + (v.w - mn)) * (1.0f / 256.0f);
         const bool bad = __ballot(!fin) != 0ull;
         if (l == 0) {
             s_min[m] = mn;
+            s_wid[m] = wid;
             s_rng[m] = (double)mx - (double)mn;
             s_abs[m] = ab;
             mins[qi * M + m] = mn;
@@ -538,15 +558,22 @@ __global__ __launch_bounds__(256) void adc_qstats_kernel(const float* __restrict
     }
     __syncthreads();
     if (threadIdx.x == 0) {
-        double base = 0.0, rng = 0.0, mag = 0.0;
+        double base = 0.0, rng = 0.0, mag = 0.0, wid = 0.0;
         for (int m = 0; m < M; ++m) {
             base += s_min[m];
             rng = fmax(rng, s_rng[m]);
             mag += s_abs[m];
+            wid = fmax(wid, s_wid[m]);
         }
         AdcQStat st;
         st.base = base;
-        st.delta = rng > 0.0 ? rng / (double)adc_qmax(M) : 1.0;
+        // the integer grid spans kAdcSpan x the largest mean offset: entries above it clamp to
+        // QMAX (a clamped q still has q delta <= lut - min, so every bound stays a lower bound),
+        // and the rows near the top -- small entries in most subspaces -- get a finer grid than
+        // the full range would give (round 5: range / 255 certified too few queries on
+        // k-means codebooks, whose far centroids stretch the range)
+        const double span = fmin(rng, kAdcSpan * wid);
+        st.delta = span > 0.0 ? span / (double)adc_qmax(M) : (rng > 0.0 ? rng / (double)adc_qmax(M) : 1.0);
         // fp32 canonical sum: |fl(sum) - sum| <= gamma_{M-1} sum |t| <= gamma_M mag; 2x that, plus
         // fp64 slack for base and delta * S
         st.margin = 2.0 * (double)M * 5.9604644775390625e-8 * mag + 1e-12 * (mag + fabs(base));
@@ -639,9 +666,12 @@ __global__ __launch_bounds__(kScanWaves * 64) void adc_qscan_kernel(
     }
     __syncthreads();
 
-    uint32_t m1[QB], m2[QB];  // per query: the lane's two smallest (S << 16 | step), ~0u = none
+    // per query: the lane's kLaneKeys smallest keys (S << 16 | step) in increasing order, ~0u = none
+    uint32_t mk[kLaneKeys][QB];
 #pragma unroll
-    for (int qq = 0; qq < QB; ++qq) m1[qq] = m2[qq] = 0xFFFFFFFFu;
+    for (int t = 0; t < kLaneKeys; ++t)
+#pragma unroll
+        for (int qq = 0; qq < QB; ++qq) mk[t][qq] = 0xFFFFFFFFu;
 
     const int64_t rbeg = (int64_t)blockIdx.x * chunk_rows;
     const int64_t rend = min(n, rbeg + chunk_rows);
@@ -652,6 +682,10 @@ __global__ __launch_bounds__(kScanWaves * 64) void adc_qscan_kernel(
 #pragma unroll
         for (int c = 0; c < MC; ++c) cw[c] = row < rend ? cr[c] : make_uint4(0u, 0u, 0u, 0u);
     };
+    // entries of kAdcBits < 8 bits: 2^(8 - bits) lookups add up in the bytes themselves (no carry
+    // crosses a byte) before one unpack to the u16 pairs
+    constexpr int UNP = 1 << (8 - kAdcBits);
+    static_assert(UNP == 1 || UNP == 2 || UNP == 4, "entry bits");
     const int64_t first = rbeg + (int64_t)wv * 64;
     fetch(first + lane);
     uint32_t step = 0;
@@ -674,6 +708,7 @@ __global__ __launch_bounds__(kScanWaves * 64) void adc_qscan_kernel(
         for (int jw = 0; jw < 4 * MC; ++jw) {
             const uint32_t wrd = wq[0];
             const uint32_t wofs = tbase + (uint32_t)jw * (4u * 256u * 4u * NWD);
+            uint32_t a8[4] = {0u, 0u, 0u, 0u};  // byte sums of up to UNP lookups
 #pragma unroll
             for (int b = 0; b < 4; ++b) {
                 uint32_t cb, o1;
@@ -682,9 +717,13 @@ __global__ __launch_bounds__(kScanWaves * 64) void adc_qscan_kernel(
                 const u32x4v t0 = *(reinterpret_cast<const lds_u4*>((uintptr_t)o1) + b * 256);
                 const uint32_t tv[4] = {t0.x, t0.y, t0.z, t0.w};
 #pragma unroll
-                for (int wd = 0; wd < 4; ++wd) {  // bytes (4w, 4w+2, 4w+1, 4w+3) -> u16 pairs
-                    acc[2 * wd] += __builtin_amdgcn_perm(tv[wd], tv[wd], 0x0C020C00u);
-                    acc[2 * wd + 1] += __builtin_amdgcn_perm(tv[wd], tv[wd], 0x0C030C01u);
+                for (int wd = 0; wd < 4; ++wd) a8[wd] = (b % UNP == 0) ? tv[wd] : a8[wd] + tv[wd];
+                if ((b + 1) % UNP == 0) {
+#pragma unroll
+                    for (int wd = 0; wd < 4; ++wd) {  // bytes (4w, 4w+2, 4w+1, 4w+3) -> u16 pairs
+                        acc[2 * wd] += __builtin_amdgcn_perm(a8[wd], a8[wd], 0x0C020C00u);
+                        acc[2 * wd + 1] += __builtin_amdgcn_perm(a8[wd], a8[wd], 0x0C030C01u);
+                    }
                 }
             }
 #pragma unroll
@@ -692,50 +731,58 @@ __global__ __launch_bounds__(kScanWaves * 64) void adc_qscan_kernel(
         }
         // a row past the chunk takes part in nothing (the last step only)
         const uint32_t inval = row < rend ? 0u : 0xFFFFFFFFu;
+        auto insert = [&](int qq, uint32_t key) __attribute__((always_inline)) {
+            // sorted insert into (m0 <= m1 [<= m2]): med3 / min per slot
+            if constexpr (kLaneKeys == 3) mk[2][qq] = umed3(mk[1][qq], mk[2][qq], key);
+            mk[1][qq] = umed3(mk[0][qq], mk[1][qq], key);
+            mk[0][qq] = min(mk[0][qq], key);
+        };
 #pragma unroll
         for (int j = 0; j < NACC; ++j) {
-            const uint32_t klo = ((acc[j] << 16) | step) | inval;          // query 2j
-            const uint32_t khi = ((acc[j] & 0xFFFF0000u) | step) | inval;  // query 2j + 1
-            m2[2 * j] = umed3(m1[2 * j], m2[2 * j], klo);
-            m1[2 * j] = min(m1[2 * j], klo);
-            m2[2 * j + 1] = umed3(m1[2 * j + 1], m2[2 * j + 1], khi);
-            m1[2 * j + 1] = min(m1[2 * j + 1], khi);
+            insert(2 * j, ((acc[j] << 16) | step) | inval);                // query 2j
+            insert(2 * j + 1, ((acc[j] & 0xFFFF0000u) | step) | inval);    // query 2j + 1
         }
     }
-    // per query: select the candidates below T, the bound B, write K1 slots
+    // per query: select the candidates below T, the bound B, write K1 slots.  A lane's unlisted
+    // rows have keys >= its last kept key, so B = min(T, min over lanes of that key's S).
     const int64_t part = (int64_t)blockIdx.x * kScanWaves + wv;
     const uint64_t below = (1ull << lane) - 1ull;
 #pragma unroll
     for (int qq = 0; qq < QB; ++qq) {
         if (qq >= nqb) continue;
-        const uint32_t s1 = m1[qq] >> 16, s2 = m2[qq] >> 16;  // 0xFFFF: no candidate
+        uint32_t sv[kLaneKeys];
+#pragma unroll
+        for (int t = 0; t < kLaneKeys; ++t) sv[t] = mk[t][qq] >> 16;  // 0xFFFF: no candidate
         // T: the largest t in [0, 0xFFFF] with #{candidates with S < t} <= k1
         uint32_t lo = 0, hi = 0xFFFF;  // keys of rows past the chunk have S = 0xFFFF: never candidates
         while (lo < hi) {  // wave-uniform
             const uint32_t mid = (lo + hi + 1) >> 1;
-            const int cnt = __popcll(__ballot(s1 < mid)) + __popcll(__ballot(s2 < mid));
+            int cnt = 0;
+#pragma unroll
+            for (int t = 0; t < kLaneKeys; ++t) cnt += __popcll(__ballot(sv[t] < mid));
             if (cnt <= k1) lo = mid; else hi = mid - 1;
         }
         const uint32_t T = lo;
-        // min over lanes of the second key's S (ballot binary search: the largest t with no s2 < t)
-        uint32_t blo = 0, bhi = 0xFFFF;
+        uint32_t blo = 0, bhi = 0xFFFF;  // min over lanes of the last kept key's S
         while (blo < bhi) {
             const uint32_t mid = (blo + bhi + 1) >> 1;
-            if (__ballot(s2 < mid) == 0ull) blo = mid; else bhi = mid - 1;
+            if (__ballot(sv[kLaneKeys - 1] < mid) == 0ull) blo = mid; else bhi = mid - 1;
         }
         const uint32_t B = min(T, blo);
         float* od = part_d + (part * nq + q0 + qq) * k1;
         uint32_t* oi = part_i + (part * nq + q0 + qq) * k1;
-        const bool t1 = s1 < T, t2 = s2 < T;
-        const uint64_t b1 = __ballot(t1), b2 = __ballot(t2);
-        const int n1 = __popcll(b1);
-        const int p1 = __popcll(b1 & below), p2 = n1 + __popcll(b2 & below);
-        auto rid = [&](uint32_t key) {
-            return (uint32_t)(id_offset + first + (int64_t)(key & 0xFFFFu) * (kScanWaves * 64) + lane);
-        };
-        if (t1) { od[p1] = (float)s1; oi[p1] = rid(m1[qq]); }
-        if (t2) { od[p2] = (float)s2; oi[p2] = rid(m2[qq]); }
-        const int used = n1 + __popcll(b2);
+        int used = 0;
+#pragma unroll
+        for (int t = 0; t < kLaneKeys; ++t) {
+            const bool take = sv[t] < T;
+            const uint64_t bt = __ballot(take);
+            if (take) {
+                const int at = used + __popcll(bt & below);
+                od[at] = (float)sv[t];
+                oi[at] = (uint32_t)(id_offset + first + (int64_t)(mk[t][qq] & 0xFFFFu) * (kScanWaves * 64) + lane);
+            }
+            used += __popcll(bt);
+        }
         for (int e = used + lane; e < k1; e += 64) { od[e] = INFINITY; oi[e] = kNoId; }
         // B = 0xFFFF: every row of the part is listed
         if (lane == 0) part_b[part * nq + q0 + qq] = B >= 0xFFFFu ? INFINITY : (float)B;
@@ -1159,6 +1206,13 @@ extern "C" int mivq_adc_search(const float* lut, int64_t nq, const uint8_t* code
         if (e != hipSuccess) return set_error(MIVQ_ERR_HIP, "adc_search (filtered): %s", hipGetErrorString(e));
         qcount = reinterpret_cast<const int*>(ws + FL.fail);
         qlist = qcount + 1;
+        if (const char* sv = getenv("MIVQ_ADC_STATS"); sv && atoi(sv) != 0) {  // profiling: blocking
+            int cnt = -1;
+            if (hipMemcpyAsync(&cnt, qcount, sizeof(int), hipMemcpyDeviceToHost, st) == hipSuccess &&
+                hipStreamSynchronize(st) == hipSuccess)
+                fprintf(stderr, "mivq_adc_search: %d of %lld queries not certified (re-run on the fp32 scan)\n", cnt,
+                        (long long)nq);
+        }
         if (no_fallback) return MIVQ_OK;
     }
     const int64_t nch = filtered ? nch_fb : nch_exact;

@@ -77,8 +77,23 @@ def exchange_topk(d: torch.Tensor, i: torch.Tensor, k: int,
     dist.all_gather_into_tensor(gd, d.contiguous())
     dist.all_gather_into_tensor(gi, i.contiguous())
     gd, gi = gd.to(home), gi.to(home)
+    if merge is None and k > 256:
+        merge = _merge_sorted_large  # mivq_topk_merge keeps its lists in one wave (k <= 256)
     merge = merge or _native.topk_merge
     return merge(gd.view(world, nq, k), gi.view(world, nq, k), k)
+
+
+def _merge_sorted_large(gd: torch.Tensor, gi: torch.Tensor, k: int) -> Tuple[torch.Tensor, torch.Tensor]:
+    """(parts, nq, k) lists -> (nq, k) by (dist, uint32 id), NaN as +inf: two stable sorts."""
+    parts, nq, _ = gd.shape
+    d = gd.permute(1, 0, 2).reshape(nq, parts * k)
+    i = gi.permute(1, 0, 2).reshape(nq, parts * k)
+    d = torch.where(torch.isnan(d), torch.full_like(d, float("inf")), d)
+    iu = i.to(torch.int64) & 0xFFFFFFFF
+    o1 = torch.argsort(iu, dim=1, stable=True)
+    d1, i1 = torch.gather(d, 1, o1), torch.gather(i, 1, o1)
+    o2 = torch.argsort(d1, dim=1, stable=True)[:, :k]
+    return torch.gather(d1, 1, o2).contiguous(), torch.gather(i1, 1, o2).contiguous()
 
 
 def broadcast_quantizer(model: Optional[BaseQuantizer], src: int = 0) -> BaseQuantizer:

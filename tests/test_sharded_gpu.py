@@ -54,7 +54,7 @@ def test_streaming_sweep_two_ranks_one_gpu(dev, tmp_path):
     assert m1["total_vectors_compressed"] == m2["total_vectors_compressed"] == 20003
     assert m1["num_batches"] == m2["num_batches"] == 7
     assert m1["mse"] == m2["mse"]  # bit for bit
-    assert m1["n_gpus"] == 1 and m2["n_gpus"] == 2 and c2["n_gpus"] == 2 and c2["M"] == 8
+    assert m1["n_gpus"] == 1 and m2["n_gpus"] == 2 and c1 == c2 == {"M": 8, "B": 8}  # the reference's config
     for m in (m1, m2):
         assert m["device"] and 0.0 < m["roofline_frac"] < 1.0 and m["encode_vectors_per_s"] > 0
 
@@ -91,5 +91,31 @@ def test_sweep_logs_device_fields(dev, tmp_path):
           with_recall=False, with_pairwise=False, with_rank=False, num_pairs=10, rank_k=10, ground_truth_path=None,
           codebooks_dir=str(tmp_path / "cb"), db_path=str(db), gpus=1, device=None)
     (m, c, _), = _rows(db)
-    assert m["n_gpus"] == 1 and c["n_gpus"] == 1 and m["device"] == c["device"]
+    assert m["n_gpus"] == 1 and m["device"] and "n_gpus" not in c  # config_json: the reference's grid config
     assert m["encode_device_ms"] > 0 and 0.0 < m["roofline_frac"] < 1.0
+
+
+@pytest.mark.gpu
+def test_sweep_two_ranks_deal_configs(dev, tmp_path):
+    """`vq-benchmark sweep --gpus 2`: the grid's configurations go to the ranks round-robin, every
+    configuration is logged once under one sweep id, and each row equals the single-process
+    run of the same configuration (codes and metrics are deterministic)."""
+    base = [sys.executable, "-u", "-m", "haag_vq", "sweep", "--method", "pq", "--dataset", "dummy",
+            "--num-samples", "3000", "--dim", "64", "--pq-subquantizers", "4,8,16", "--pq-bits", "8",
+            "--no-with-recall", "--no-with-pairwise", "--no-with-rank", "--codebooks-dir", str(tmp_path / "cb")]
+    out = {}
+    for g in (1, 2):
+        db = tmp_path / f"sweep{g}.db"
+        p = subprocess.run(base + ["--db-path", str(db), "--gpus", str(g)], capture_output=True, text=True,
+                           env=_env(), timeout=300, cwd=str(tmp_path))
+        assert p.returncode == 0, p.stdout[-3000:] + p.stderr[-3000:]
+        out[g] = _rows(db)
+    assert len(out[1]) == len(out[2]) == 3
+    assert len({sid for _, _, sid in out[2]}) == 1  # one sweep id across the ranks
+    one = {c["subquantizers"]: m for m, c, _ in out[1]}
+    two = {c["subquantizers"]: m for m, c, _ in out[2]}
+    assert set(one) == set(two) == {4, 8, 16}
+    for M in one:
+        assert two[M]["n_gpus"] == 2 and one[M]["n_gpus"] == 1
+        assert two[M]["reconstruction_distortion"] == one[M]["reconstruction_distortion"]
+        assert two[M]["compression_ratio"] == one[M]["compression_ratio"]

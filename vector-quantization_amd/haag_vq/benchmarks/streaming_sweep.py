@@ -234,7 +234,6 @@ def streaming_sweep(
                # time / (8 TB/s x GPUs): the fraction of the node's HBM roofline
                "roofline_frac": (total * (4 * dim + code_bytes) / enc_s / (8.0e12 * info.world)
                                  if enc_s > 0 else None)}
-    config = dict(config, n_gpus=info.world, device=metrics["device"])
     if head:
         log_run(method=method, dataset=f"{dataset}-streaming", metrics=metrics, config=config, sweep_id=sweep_id,
                 db_path=db_path)

@@ -243,9 +243,9 @@ def _run_single_config(method: str, dataset: str, data: Dataset, config: Dict[st
                        with_pairwise: bool, with_rank: bool, num_pairs: int, rank_k: int, sweep_id: str = None,
                        codebooks_dir: Path = None, db_path: str = None, n_gpus: int = 1) -> Dict[str, Any]:
     """Fit, encode, decode and score one configuration; log it; return its metrics.  Besides
-    the reference's fields, metrics_json carries ``device``, ``encode_device_ms`` and
-    ``roofline_frac`` (the device encode of X against the 8 TB/s HBM roofline) and config_json
-    ``n_gpus`` and ``device``."""
+    the reference's fields, metrics_json carries ``device``, ``n_gpus``, ``encode_device_ms`` and
+    ``roofline_frac`` (the device encode of X against the 8 TB/s HBM roofline, SURVEY §5);
+    config_json stays the reference's grid config."""
     model = _build_model(method, config)
     X = data.vectors
     t0 = perf_counter()
@@ -279,7 +279,6 @@ def _run_single_config(method: str, dataset: str, data: Dataset, config: Dict[st
         metrics.update(evaluate_recall(data, model, num_queries=100))
     metrics.update(device_encode_roofline(model, X))
     metrics["n_gpus"] = int(n_gpus)
-    config = dict(config, n_gpus=int(n_gpus), device=metrics.get("device"))
 
     log_run(method=method, dataset=dataset, metrics=metrics, config=config, sweep_id=sweep_id, db_path=db_path)
 

@@ -84,5 +84,9 @@ def test_no_packed_fp32_on_lds_loads():
 
     from haag_vq import _native
 
-    findings = isa_audit.audit(Path(_native.LIB_PATH))
+    walked = []
+    findings = isa_audit.audit(Path(_native.LIB_PATH), walked)
+    for k in ("pq_encode_cs_kernel", "pq_resolve_merged_kernel", "adc_lut_kernel", "adc_qscan_kernel",
+              "adc_rerank_kernel", "opq_split_gemm_kernel", "pairwise_kernel"):
+        assert any(k in w for w in walked), (k, len(walked))  # the audit really read the library
     assert not findings, {k[:80]: v[:2] for k, v in findings.items()}

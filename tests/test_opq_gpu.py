@@ -56,6 +56,35 @@ def test_split_gemm_vs_fp64(dev, n, d, transpose):
     _check(y, X, A if transpose else A.T)
 
 
+@pytest.mark.parametrize("d", [1536, 288])
+def test_split_gemm_row_scales_along_k(dev, d):
+    """Per-row power-of-two scales against rows whose magnitude changes along k: growing 4x per
+    32-dim K step, starting with zeros or with tiny values, nonzero only in the last dim,
+    decreasing, one loud chunk mid-row -- next to ordinary rows of the same tile, both tile
+    shapes (round 5 also measured scales found chunk by chunk inside the GEMM against these)."""
+    from haag_vq import _native
+
+    rng = np.random.default_rng(d)
+    n = 300
+    X = rng.standard_normal((n, d)).astype(np.float32)
+    k = np.arange(d)
+    X[10] *= (2.0 ** (2 * (k // 32) % 60)).astype(np.float32)   # grows 4x per chunk (wraps)
+    X[11, :100] = 0.0
+    X[11, 100:] *= 1e-30
+    X[12, :32] *= 1e-30
+    X[12, 32:] *= 1e30                                            # factor 2^-200: early terms vanish
+    X[13, : d // 2] = 0.0
+    X[14, :-1] = 0.0
+    X[15] *= (2.0 ** -((k // 32) % 40)).astype(np.float32)        # decreasing
+    X[16, 64:96] *= 1e6                                           # one loud chunk mid-row
+    X[200] = X[10] * np.float32(1e-10)                            # the same pattern in another wave's rows
+    A = _orth(d, d + 1)
+    for transpose in (False, True):
+        prep = _native.opq_prepare(_t(A, dev), transpose)
+        y = _native.opq_rotate_prepared(_t(X, dev), prep).cpu().numpy()
+        _check(y, X, A if transpose else A.T)
+
+
 def test_split_gemm_chunk_boundary(dev):
     """More rows than one GEMM chunk (2^20 rows: the f16 planes of x are built per chunk):
     rows on both sides of the boundary and the ragged end match fp64."""
@@ -155,12 +184,16 @@ def test_polar_factor_newton_schulz(dev):
     V, _ = np.linalg.qr(rng.standard_normal((d, d)))
     S = np.logspace(0, -4, d)
     G = (U * S) @ V.T
-    Q = polar_factor(_t(G, dev)).cpu().numpy()
+    info = {}
+    Q = polar_factor(_t(G, dev), info=info).cpu().numpy()
+    assert info["path"] == "newton-schulz", info
     np.testing.assert_allclose(Q, U @ V.T, atol=1e-9)
     np.testing.assert_allclose(Q.T @ Q, np.eye(d), atol=1e-12)
     S[-3:] = 0.0  # rank deficient: Newton-Schulz keeps the zero singular values -> fallback
     Gd = (U * S) @ V.T
-    Qd = polar_factor(_t(Gd, dev)).cpu().numpy()
+    info = {}
+    Qd = polar_factor(_t(Gd, dev), info=info).cpu().numpy()
+    assert info["path"] == "svd" and info["iters"] < 45, info  # the stall is seen early
     np.testing.assert_allclose(Qd.T @ Qd, np.eye(d), atol=1e-10)
     np.testing.assert_allclose(Qd @ (Qd.T @ Gd), Gd, atol=1e-10)
 

@@ -43,6 +43,9 @@ def _sweep(tmp_path, *args):
     return [(m, d, json.loads(mj), json.loads(cj), sid) for m, d, mj, cj, sid in rows]
 
 
+DEVICE_FIELDS = {"device", "n_gpus", "encode_device_ms", "roofline_frac"}
+
+
 def test_sweep_pq_m8_b8_dummy(tmp_path, kat):
     rows = _sweep(tmp_path, "--method", "pq", "--pq-subquantizers", "8", "--pq-bits", "8")
     assert len(rows) == 1
@@ -51,7 +54,9 @@ def test_sweep_pq_m8_b8_dummy(tmp_path, kat):
     assert (method, dataset) == ("pq", "dummy")
     assert config == ref["config"]
     assert sid.startswith("sweep_")
-    assert set(metrics) == set(ref["metrics"])
+    # the reference's fields, plus the device fields this build adds (sweep.py)
+    assert set(metrics) == set(ref["metrics"]) | DEVICE_FIELDS
+    assert metrics["n_gpus"] == 1 and metrics["device"] and 0.0 < metrics["roofline_frac"] < 1.0
     assert metrics["compression_ratio"] == ref["metrics"]["compression_ratio"] == 512.0
     assert metrics["reconstruction_distortion"] == pytest.approx(ref["metrics"]["reconstruction_distortion"], rel=0.03)
     assert metrics["rank_distortion@10"] == pytest.approx(1.0 - metrics["recall@10"])

@@ -21,6 +21,7 @@ for group in "FETCH_SIZE" "WRITE_SIZE" \
     if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then exit $rc; fi
 done
 python tools/traffic.py $OUT 3 > $OUT/traffic.log 2>&1
-for k in pq_encode_cs_kernelILi6ELi3ELi0ELi96 pq_resolve_merged_kernelILi6ELi96 pq_encode_cs_kernelILi12ELi3ELi0ELi192 pq_encode_cs_kernelILi3ELi3ELi0ELi48 opq_split_gemm_kernel sq_encode_f32_vec_kernel rabitq_encode_wide_kernel erq_rotate_fast_kernel; do
+for k in pq_encode_cs_kernelILi6ELi3ELi96 pq_resolve_merged_kernelILi6ELi96 pq_encode_cs_kernelILi12ELi3ELi192 pq_encode_cs_kernelILi3ELi3ELi48 opq_split_gemm_kernel sq_encode_f32_vec_kernel rabitq_encode_wide_kernel erq_rotate_fast_kernel; do
     echo "== $k"; python tools/pmc_summary.py $OUT $k 3
 done > $OUT/summary.txt 2>&1
+cp profiles/traffic.json $OUT/traffic.json

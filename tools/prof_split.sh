@@ -15,3 +15,7 @@ f=$(ls $OUT/*/run_kernel_trace.csv 2>/dev/null | head -1); [ -z "$f" ] && f=$(ls
 python tools/ktrace.py $f pq_encode_cs_kernel pq_resolve transpose_codes adc_lut adc_scan topk_merge | tee $OUT/split.txt
 s=$(ls $OUT/*/run_kernel_stats.csv 2>/dev/null | head -1); [ -z "$s" ] && s=$(ls $OUT/run_kernel_stats.csv)
 cp $s $OUT/kernel_stats.csv
+# every kernel instance (template arguments) by launch size: the 2^21-row slices, the tail, the
+# small calls of the fit and the sweep, each on its own line
+for k in pq_ adc_ topk_ opq_ sq_ rabitq_; do python tools/ktrace_v.py $f $k; done > $OUT/split_by_grid.txt
+python tools/ktrace_calls.py $f > $OUT/split_by_call.txt

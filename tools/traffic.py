@@ -18,11 +18,11 @@ from pmc_select import select  # noqa: E402
 
 # workload -> kernel-name substrings (template arguments select the shape)
 WORKLOADS = {
-    "pq16_encode_1000000x1536_gaussian": ["pq_encode_cs_kernelILi6ELi3ELi0ELi96", "pq_resolve_merged_kernelILi6ELi96",
+    "pq16_encode_1000000x1536_gaussian": ["pq_encode_cs_kernelILi6ELi3ELi96", "pq_resolve_merged_kernelILi6ELi96",
                                           "pq_transpose_codes16_kernel<16>"],
     # the sweep's PQ8 shape (dsub 192): filter + resolve (its transpose kernel, <0>, is shared
     # with the OPQ32 encode that runs after it, so its last dispatches are not this leg's)
-    "pq8_encode_1000000x1536": ["pq_encode_cs_kernelILi12ELi3ELi0ELi192", "pq_resolve_merged_kernelILi12ELi192"],
+    "pq8_encode_1000000x1536": ["pq_encode_cs_kernelILi12ELi3ELi192", "pq_resolve_merged_kernelILi12ELi192"],
     "opq32_rotate_1000000x1536": ["opq_row_scale_kernel", "opq_split_gemm_kernel"],
     "sq8_encode_1000000x3072": ["sq_encode_f32_vec_kernel"],
     "rabitq1_encode_1000000x3072": ["rabitq_encode_wide_kernel"],  # d % 512 == 0 (rabitq.hip)

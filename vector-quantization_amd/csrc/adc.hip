@@ -470,23 +470,25 @@ __global__ __launch_bounds__(256) void topk_merge_kernel(const float* __restrict
 // Filtered ADC search (M = 16 / 32, ksub = 256): the same canonical fp32 top-k, found in two
 // passes.
 //
-// 1. adc_qstats_kernel / adc_qtab_kernel quantise every query's LUT to integers:
-//      q[m][c] = min(QMAX, floor((lut[m][c] - min_m) / delta)),  delta = max_m range_m / QMAX,
-//    QMAX = floor(32767 / M), so a row's sum S = sum_m q[m][code_m] <= 32767 (15 bits).  Two
-//    queries share a dword (16-bit fields), 16 (M = 16) or 8 (M = 32) queries one 32 / 16-B
-//    table entry: half the LDS bytes and VALU adds per (query, row) of the fp32 table, and the
-//    adds are plain v_add_u32 (no carry can cross a field: every partial sum < 2^15).
-// 2. adc_qscan_kernel keeps, per part (workgroup chunk x wave) and query, the exact top-k of
-//    (S, id): a screen of all queries at once (SWAR: field (0x8000 + t) - S has bit 15 set iff
-//    S <= t, no borrow since S, t < 2^15) and the same wave-resident lists as the fp32 scan.
+// 1. adc_qstats_kernel / adc_qtab_kernel quantise every query's LUT to 6-bit integers:
+//      q[m][c] = min(63, floor((lut[m][c] - min_m) / delta)),  delta = min(range, 2 w) / 63
+//    (range = max_m range_m, w = the largest mean offset above min_m: the grid is fine where the
+//    rows near the top live, entries above it clamp), one byte per query, 16 queries per 16-B
+//    table entry.  A row's sum S = sum_m q[m][code_m] < 2^11 (M <= 32).
+// 2. adc_qscan_kernel: four lookups add up inside the bytes (4 x 63 < 256) before one v_perm
+//    unpack to u16 pairs, so a (query, row) costs M / 8 byte-adds + M / 4 unpacks + M / 4
+//    16-bit adds; every lane keeps, per query, the three smallest keys (S << 16 | step) of its
+//    own rows (v_med3 / v_min, registers only), and each wave ("part") finally lists the
+//    candidates below a ballot-searched threshold plus its bound B (every unlisted row of the
+//    part has S >= B).
 // 3. adc_rerank_kernel (one wave per query) evaluates the canonical fp32 distance (the sum over
 //    m in order of the fp32 LUT entries, include/mivq.h) of every listed row and keeps the exact
 //    top-k.  It is the canonical answer if no row outside the lists can beat its k-th element
-//    (E_k): a row missing from part p's full list has S >= S_k(p), and, with q*delta <=
-//    lut - min, its canonical distance is >= LB(S) = base + delta * S - margin (base = sum_m
-//    min_m, margin >= the fp32 summation error gamma_M * sum_m max_c |lut[m][c]| plus fp64
-//    slack).  So the query is certified when LB(S_k(p)) > E_k for every part p whose list is
-//    full; a query that is not (or whose LUT is not finite) is listed for
+//    (E_k): a row part p did not list has S >= B(p), and, with q*delta <= lut - min, its
+//    canonical distance is >= LB(S) = base + delta * S - margin (base = sum_m min_m, margin >=
+//    the fp32 summation error gamma_M * sum_m max_c |lut[m][c]| plus fp64 slack).  So the query
+//    is certified when LB(B(p)) > E_k for every part p; a query that is not (or whose LUT is
+//    not finite) is listed for
 // 4. the fp32 scan (adc_scan_kernel) re-run on the listed queries only (query indirection; the
 //    workgroups of empty slots return at once) and its merge.
 // Results are identical to the fp32 scan's for every input.
@@ -495,22 +497,14 @@ struct AdcQStat {
     int bad, pad;
 };
 
-// Table entries: u16 per query (QMAX = 32767 / M), or u8 (QMAX = 255, E8: half the table
-// bytes again; unpacked to the u16 fields by two v_perm_b32 per dword).
-constexpr bool kAdcE8 = true;  // u8 entries (round 5: the u16 table measured no faster per call)
-#ifndef MIVQ_AB_ADC_SPAN  // A/B builds: the integer grid's span in mean offsets
-#define MIVQ_AB_ADC_SPAN 2.0
-#endif
-constexpr double kAdcSpan = MIVQ_AB_ADC_SPAN;
-#ifndef MIVQ_AB_ADC_BITS  // A/B builds: bits per integer-table entry (8, 7 or 6)
-#define MIVQ_AB_ADC_BITS 6
-#endif
-#ifndef MIVQ_AB_ADC_KEYS  // A/B builds: keys kept per lane and query (2 or 3)
-#define MIVQ_AB_ADC_KEYS 3
-#endif
-constexpr int kAdcBits = MIVQ_AB_ADC_BITS;
-constexpr int kLaneKeys = MIVQ_AB_ADC_KEYS;
-__host__ __device__ constexpr int adc_qmax(int M) { return kAdcE8 ? (1 << kAdcBits) - 1 : 32767 / M; }
+// Integer table: 6-bit entries in bytes (round 5, A/B-measured against 8- and 7-bit entries and
+// u16 entries: 6 bits lets four lookups share one unpack, and certified as many queries once the
+// grid span followed the mean offset); lanes keep 3 keys per query (2 left ~2 % of the queries
+// uncertified on Gaussian rows, 3 none).
+constexpr int kAdcBits = 6;
+constexpr int kLaneKeys = 3;
+constexpr double kAdcSpan = 2.0;  // the grid's span in mean offsets above the minimum
+__host__ __device__ constexpr int adc_qmax(int) { return (1 << kAdcBits) - 1; }
 
 __device__ __forceinline__ float wave_min(float v) {
 #pragma unroll
@@ -583,8 +577,7 @@ __global__ __launch_bounds__(256) void adc_qstats_kernel(const float* __restrict
     }
 }
 
-// grid (ceil(nq / QB), M), block 256 (code c): table block b = (M, 256, NWD) dwords.  u16
-// entries: query 2j in the low and 2j + 1 in the high half of dword j.  u8 entries (E8): dword
+// grid (ceil(nq / QB), M), block 256 (code c): table block b = (M, 256, QB / 4) dwords; dword
 // w holds queries (4w, 4w + 2, 4w + 1, 4w + 3) in bytes 0..3, so the two byte-pair unpacks
 // give the u16 pairs (4w, 4w + 1) and (4w + 2, 4w + 3).  q <= (lut - min) / delta (the ratio
 // is shrunk by 2^-50 before the floor, so fp64 rounding never rounds it up past an integer).
@@ -592,7 +585,7 @@ template <int QB>
 __global__ __launch_bounds__(256) void adc_qtab_kernel(const float* __restrict__ lut, int64_t nq, int M,
                                                        const float* __restrict__ mins,
                                                        const AdcQStat* __restrict__ qs, uint32_t* __restrict__ tab) {
-    constexpr int NWD = kAdcE8 ? QB / 4 : QB / 2;
+    constexpr int NWD = QB / 4;
     const int64_t qb = blockIdx.x;
     const int m = blockIdx.y, c = threadIdx.x;
     const int qmax = adc_qmax(M);
@@ -611,12 +604,8 @@ __global__ __launch_bounds__(256) void adc_qtab_kernel(const float* __restrict__
                 v = x >= (double)qmax ? (uint32_t)qmax : x > 0.0 ? (uint32_t)floor(x) : 0u;
             }
         }
-        if constexpr (kAdcE8) {
-            const int r = qq & 3;
-            w[qq >> 2] |= v << (8 * (((r & 1) << 1) | (r >> 1)));
-        } else {
-            w[qq >> 1] |= v << (16 * (qq & 1));
-        }
+        const int r = qq & 3;
+        w[qq >> 2] |= v << (8 * (((r & 1) << 1) | (r >> 1)));
     }
     uint32_t* dst = tab + ((qb * M + m) * 256 + c) * NWD;
     if constexpr (NWD >= 4) {
@@ -627,15 +616,15 @@ __global__ __launch_bounds__(256) void adc_qtab_kernel(const float* __restrict__
     }
 }
 
-// grid (nchunks, ceil(nq / 16)), block kScanWaves waves (the fp32 scan's structure): the u8
+// grid (nchunks, ceil(nq / 16)), block kScanWaves waves (the fp32 scan's structure): the byte
 // tables of 16 queries in LDS (M * 4 KiB), M = 16 MC, each lane one row per wave-step with its
 // code row loaded a step ahead.  No wave-level list during the scan: every lane keeps, per
-// query, the two smallest keys (S << 16 | wave-step) of its own rows (v_med3 + v_min per row
-// and query, registers only).  At the end each wave ("part") selects from its 128 lane
+// query, the kLaneKeys smallest keys (S << 16 | wave-step) of its own rows (v_med3 + v_min per
+// row and query, registers only).  At the end each wave ("part") selects from its 192 lane
 // candidates per query those with S below T = the largest value with at most K1 candidates
 // below it (binary search on ballot counts), writes them (float(S), id) -- the rest of the K1
-// slots sentinels -- and its bound B = min(T, min over lanes of the lane's second key's S):
-// every row of the part that is not listed has S >= B (a lane's other rows are >= its second
+// slots sentinels -- and its bound B = min(T, min over lanes of the lane's last key's S): every
+// row of the part that is not listed has S >= B (a lane's other rows are >= its last kept
 // key, a dropped candidate is >= T).  (The round-5 first cut kept wave-resident exact lists
 // updated by ballot + shuffle inserts: those inserts were most of its LDS instructions.)
 constexpr int kQB = 16;  // queries per integer-table block
@@ -988,7 +977,7 @@ AdcFilteredLayout adc_filtered_layout(int64_t nq, int64_t n, int M, int k, size_
     L.parts = L.nch * kScanWaves;
     L.stats = off;  off = align_up(off + (size_t)nq * sizeof(AdcQStat), 256);
     L.mins = off;   off = align_up(off + (size_t)nq * M * sizeof(float), 256);
-    L.tab = off;    off = align_up(off + (size_t)ceil_div(nq, QB) * M * 256 * QB * (kAdcE8 ? 1 : 2), 256);
+    L.tab = off;    off = align_up(off + (size_t)ceil_div(nq, QB) * M * 256 * QB, 256);
     L.p1d = off;    off = align_up(off + (size_t)L.parts * nq * L.k1 * sizeof(float), 256);
     L.p1i = off;    off = align_up(off + (size_t)L.parts * nq * L.k1 * sizeof(uint32_t), 256);
     L.p1b = off;    off = align_up(off + (size_t)L.parts * nq * sizeof(float), 256);

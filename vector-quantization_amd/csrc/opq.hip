@@ -128,10 +128,11 @@ struct SplitTile {
 };
 using TileS = SplitTile<2, 2, 2, 2>;  // 128 x 128, 256 threads, 80 KiB (two per CU)
 using TileL = SplitTile<4, 2, 2, 4>;  // 256 x 256, 512 threads, 160 KiB (half the L2 traffic per MFMA)
-// 256 x 256 with 4 waves of 128 x 128 (accumulators in AGPRs): 16 fragment reads per 48 MFMAs
-// instead of 12 per 24 (MIVQ_OPQ_TILE4).  Measured slower: 16.0 vs 14.8 ms per 1M x 1536 GEMM
-// (one wave per SIMD cannot hide the LDS and barrier latency that two do); not the default.
-using TileW = SplitTile<2, 2, 4, 4>;
+// Measured and removed: 256 x 256 with 4 waves of 128 x 128 (16.0 vs 14.8 ms per
+// 1M x 1536 GEMM), a 4-wave software-pipelined kernel with sched_group_barrier interleaving
+// (17.4 vs 16.2 ms), non-temporal x / B-image loads, and (round 5) row scales found inside the
+// GEMM chunk by chunk instead of the row-scale pass (15.40 vs 14.65 ms: the per-chunk max and
+// its 8-lane reduction in the staging cost more than the pass over x).
 
 // Power-of-two scale 2^(14 - E) with max|v| = m 2^E, m in [0.5, 1); 1 for 0 / inf / NaN.
 // Clamped to fp32's normal exponents (rows below 2^-112 lose relative accuracy).
@@ -219,34 +220,13 @@ __global__ __launch_bounds__(256) void opq_split_b_kernel(const float* __restric
     bimg[dd + e] = lo;
 }
 
-#ifndef MIVQ_OPQ_XNT
-#define MIVQ_OPQ_XNT 0
-#endif
-#ifndef MIVQ_OPQ_BUF
-#define MIVQ_OPQ_BUF 1
-#endif
-#ifndef MIVQ_OPQ_SFIRST  // split-and-store of step s + 1 before step s's MFMAs (14.80 -> 14.27 ms, r04_s22)
-#define MIVQ_OPQ_SFIRST 1
-#endif
-#ifndef MIVQ_OPQ_UNCOND  // profiling: the loop's load / store without the last-step branches
-#define MIVQ_OPQ_UNCOND 0
-#endif
-typedef float f32x4nt __attribute__((ext_vector_type(4)));
-typedef unsigned int u32x4nt __attribute__((ext_vector_type(4)));
-#ifndef MIVQ_OPQ_BNT
-#define MIVQ_OPQ_BNT 0
-#endif
-
 // LDS staging line (x row / B column) of staging thread-slot e, 8 slots of 8 B per 64-B line.
 // A 16-lane ds_write_b64 group (or 8-lane ds_write_b128 group) covers two lines; with the 80-B
 // pitch lines j and j + 1 overlap on 4 of the 32 store banks ((a/4) mod 32: 2-way conflicts on
 // every staging store -- the ~577 M conflict cycles per 1M x 1536 rotation in PMC), lines j and
-// j + 4 do not (80 B x 4 = 16 banks apart).  MIVQ_OPQ_WSWZ = 0: the round-3 order (line e / 8); measured 16.16 -> 16.01 ms per rotation.
-#ifndef MIVQ_OPQ_WSWZ
-#define MIVQ_OPQ_WSWZ 1
-#endif
+// j + 4 do not (80 B x 4 = 16 banks apart).  Against the round-3 order (line e / 8): 16.16 ->
+// 16.01 ms per rotation.
 __device__ __forceinline__ int stage_line(int e) {
-    if (!MIVQ_OPQ_WSWZ) return e >> 3;
     const int g = e >> 4, sub = (e >> 3) & 1;
     return (g >> 2) * 8 + (g & 3) + 4 * sub;
 }
@@ -336,10 +316,10 @@ __global__ __launch_bounds__(WR * WC * 64) void opq_split_gemm_kernel(const floa
     }
     float4 xv[U];
     uint4 bv[U];
-    // MIVQ_OPQ_BUF: range-checked 16-B buffer loads (rows past n read zeros; a chunk past d gets
-    // an out-of-range offset) instead of one guarded load per chunk, which compiled to a branch
-    // per load (15.93 -> 14.80 ms per 1M x 1536 rotation, profiles/r04_s14); 32-bit offsets
-    // from the tile's first row (4 d^2 < 2^31 checked at launch)
+    // range-checked 16-B buffer loads (rows past n read zeros; a chunk past d gets an
+    // out-of-range offset) instead of one guarded load per chunk, which compiled to a branch per
+    // load (15.93 -> 14.80 ms per 1M x 1536 rotation, profiles/r04_s14); 32-bit offsets from the
+    // tile's first row (4 d^2 < 2^31 checked at launch)
     constexpr int kOob = (int)0x80000000u;
     const int trows = (int)(n - r0 < TM ? n - r0 : TM);
     const __amdgpu_buffer_rsrc_t xrs =
@@ -348,34 +328,11 @@ __global__ __launch_bounds__(WR * WC * 64) void opq_split_gemm_kernel(const floa
     auto gload = [&](int k0) __attribute__((always_inline)) {
 #pragma unroll
         for (int u = 0; u < U; ++u) {
-            if (MIVQ_OPQ_BUF) {
-                const int k = k0 + xk[u], gc = c0 + bcol[u], kb = k0 + bk[u];
-                const int vx = k < d ? (xrow[u] * d + k) * 4 : kOob;
-                const int vb = (gc < d && kb < d) ? (int)((bpl[u] * dd + (int64_t)gc * d + kb) * 2) : kOob;
-                xv[u] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(xrs, vx, 0, 0));
-                bv[u] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(brs, vb, 0, 0));
-                continue;
-            }
-            const int64_t gr = r0 + xrow[u];
-            const int k = k0 + xk[u];
-            // MIVQ_OPQ_XNT / _BNT (profiling): non-temporal loads of x / of the B image
-            const float* xp = x + gr * d + k;
-            if (MIVQ_OPQ_XNT) {
-                const f32x4nt v = (gr < n && k < d) ? __builtin_nontemporal_load(reinterpret_cast<const f32x4nt*>(xp))
-                                                    : (f32x4nt){0.f, 0.f, 0.f, 0.f};
-                xv[u] = make_float4(v.x, v.y, v.z, v.w);
-            } else {
-                xv[u] = (gr < n && k < d) ? *reinterpret_cast<const float4*>(xp) : make_float4(0.f, 0.f, 0.f, 0.f);
-            }
-            const int gc = c0 + bcol[u], kb = k0 + bk[u];
-            const _Float16* bp = bimg + bpl[u] * dd + (int64_t)gc * d + kb;
-            if (MIVQ_OPQ_BNT) {
-                const u32x4nt v = (gc < d && kb < d) ? __builtin_nontemporal_load(reinterpret_cast<const u32x4nt*>(bp))
-                                                     : (u32x4nt){0u, 0u, 0u, 0u};
-                bv[u] = make_uint4(v.x, v.y, v.z, v.w);
-            } else {
-                bv[u] = (gc < d && kb < d) ? *reinterpret_cast<const uint4*>(bp) : make_uint4(0u, 0u, 0u, 0u);
-            }
+            const int k = k0 + xk[u], gc = c0 + bcol[u], kb = k0 + bk[u];
+            const int vx = k < d ? (xrow[u] * d + k) * 4 : kOob;
+            const int vb = (gc < d && kb < d) ? (int)((bpl[u] * dd + (int64_t)gc * d + kb) * 2) : kOob;
+            xv[u] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(xrs, vx, 0, 0));
+            bv[u] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(brs, vb, 0, 0));
         }
     };
     auto sstore = [&](unsigned char* buf) __attribute__((always_inline)) {
@@ -408,23 +365,18 @@ __global__ __launch_bounds__(WR * WC * 64) void opq_split_gemm_kernel(const floa
     const int nsteps = (d + SBK - 1) / SBK;
     gload(0);
     sstore(smem);
-    // MIVQ_OPQ_SFIRST: step s + 1's chunks (loaded during step s - 1) go to LDS at the START of
-    // step s, then step s + 2's loads are issued, then step s's MFMAs -- the loads have a whole
-    // step to land and the store no longer sits between the MFMAs and the barrier; loads past d
-    // read zeros (buffer loads), so no branch surrounds them (the last steps' stores are never read)
-    if (MIVQ_OPQ_SFIRST && MIVQ_OPQ_BUF) gload(SBK);
+    // stage first: step s + 1's chunks (loaded during step s - 1) go to LDS at the START of step
+    // s, then step s + 2's loads are issued, then step s's MFMAs -- the loads have a whole step
+    // to land and the store no longer sits between the MFMAs and the barrier (14.80 -> 14.27 ms,
+    // r04_s22); loads past d read zeros (buffer loads), so no branch surrounds them (the last
+    // steps' stores are never read)
+    gload(SBK);
     __syncthreads();
     const int fr = l & 31, fk = 16 * (l >> 5);  // fragment row / col and byte offset of its k-group
     for (int s = 0; s < nsteps; ++s) {
         unsigned char* cur = smem + (s & 1) * T::BUF;
-        if (MIVQ_OPQ_SFIRST && MIVQ_OPQ_BUF) {
-            sstore(smem + ((s + 1) & 1) * T::BUF);
-            gload((s + 2) * SBK);
-        } else if (MIVQ_OPQ_UNCOND && MIVQ_OPQ_BUF) {
-            gload((s + 1) * SBK);
-        } else if (s + 1 < nsteps) {
-            gload((s + 1) * SBK);
-        }
+        sstore(smem + ((s + 1) & 1) * T::BUF);
+        gload((s + 2) * SBK);
 #pragma unroll
         for (int kk = 0; kk < 2; ++kk) {
             half8 ah[RB], al[RB], bh[CB], bl[CB];
@@ -454,188 +406,11 @@ __global__ __launch_bounds__(WR * WC * 64) void opq_split_gemm_kernel(const floa
 #pragma unroll
                 for (int b = 0; b < CB; ++b) acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[a], bh[b], acc[a][b], 0, 0, 0);
         }
-        if (!(MIVQ_OPQ_SFIRST && MIVQ_OPQ_BUF) && (MIVQ_OPQ_UNCOND && MIVQ_OPQ_BUF || s + 1 < nsteps))
-            sstore(smem + ((s + 1) & 1) * T::BUF);
         __syncthreads();
     }
     // epilogue (the staging buffers are reused: every wave must be done with them)
     __syncthreads();
     store_tile<RB, CB>(acc, smem, w, l, r0 + wr * RB * 32, c0 + wc * CB * 32, n, d, rs, hdr[1], y);
-}
-
-// ------------------------------------------------------------ split-f16, pipelined (round 4)
-// The same arithmetic as opq_split_gemm_kernel (x_hi b_hi + x_hi b_lo + x_lo b_hi, f16 MFMAs,
-// fp32 accumulators) on a 256 x 256 tile with FOUR waves of 128 x 128 (4 x 4 blocks of
-// v_mfma_f32_32x32x16_f16 each, accumulators in AGPRs, one wave per SIMD, up to 512 registers):
-// * K steps of 16 (one MFMA K-slice): a stage is 16 KiB of x and 16 KiB of the B image, four
-//   16-B loads of each per thread, so two register sets (global -> register staging two steps
-//   ahead) fit next to the fragments; range-checked buffer loads (no lane branches);
-// * the split + LDS store of step s + 1 is interleaved with the 48 MFMAs of step s
-//   (sched_group_barrier), so its VALU and DS-write work issues in the MFMAs' shadow instead of
-//   in a phase of its own -- round 3's 8-wave kernel runs load / MFMA / split-and-store / barrier
-//   in lock step with the MFMA pipe about half busy;
-// * one barrier per K step with only lgkmcnt(0) before it: the next steps' global loads stay in
-//   flight across it (no vmcnt(0) in the loop).
-// LDS rows of 16 halves + 16 B pad (48 B): the fragment reads of a 16-lane group hit 16 distinct
-// 4-bank groups.  No LDS DMA.
-constexpr int PP_T = 256, PP_NT = 256, PP_K = 16, PP_U = 4;
-constexpr int PP_PITCH = PP_K * 2 + 16;       // bytes per LDS row
-constexpr int PP_PL = PP_T * PP_PITCH;        // one plane (x hi, x lo, B hi or B lo) of a stage
-constexpr int PP_BUF = 4 * PP_PL;             // 48 KiB per stage
-
-typedef unsigned int u32x4v __attribute__((ext_vector_type(4)));
-typedef _Float16 half2v __attribute__((ext_vector_type(2)));
-typedef float float2v __attribute__((ext_vector_type(2)));
-
-// v = s * (a, b): (hi, lo) f16 pairs packed in two dwords, hi = f16(v), lo = f16(v - hi)
-__device__ __forceinline__ void split_pair(float a, float b, float s, uint32_t& hi, uint32_t& lo) {
-    const float va = a * s, vb = b * s;
-    const half2v h = __builtin_convertvector((float2v){va, vb}, half2v);
-    const float2v hf = __builtin_convertvector(h, float2v);
-    const half2v lw = __builtin_convertvector((float2v){va - hf.x, vb - hf.y}, half2v);
-    hi = __builtin_bit_cast(uint32_t, h);
-    lo = __builtin_bit_cast(uint32_t, lw);
-}
-
-__global__ __launch_bounds__(PP_NT, 1) void opq_pp_gemm_kernel(const float* __restrict__ x, int64_t n, int d,
-                                                                 const float* __restrict__ rs,
-                                                                 const _Float16* __restrict__ bimg,
-                                                                 const float* __restrict__ hdr, float* __restrict__ y,
-                                                                 int64_t ctiles) {
-    // two LDS objects, one per stage: the compiler can then prove that the stores into the next
-    // stage never alias the fragment reads of the current one and interleave them with the MFMAs
-    __shared__ __attribute__((aligned(16))) unsigned char st0[PP_BUF];
-    __shared__ __attribute__((aligned(16))) unsigned char st1[PP_BUF];
-    const int tid = threadIdx.x, l = tid & 63;
-    const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
-    const int wr = w >> 1, wc = w & 1;
-    const int64_t t = xcd_tile(blockIdx.x, gridDim.x);
-    const int64_t r0 = (t / ctiles) * PP_T;
-    const int c0 = (int)(t % ctiles) * PP_T;
-    const int64_t dd = (int64_t)d * d;
-    const int nrows = (int)min<int64_t>(PP_T, n - r0);
-
-    // x: load u reads row xr0 + 64 u, dims k0 + xk .. +3; B: load u reads plane u >> 1, column
-    // bc0 + 128 (u & 1), dims k0 + bk .. +7
-    const int xr0 = tid >> 2, xk = 4 * (tid & 3);
-    const int bc0 = tid >> 1, bk = 8 * (tid & 1);
-    const __amdgpu_buffer_rsrc_t xsrc =
-        __builtin_amdgcn_make_buffer_rsrc((void*)(x + r0 * d), 0, (int)((int64_t)nrows * d * 4), 0x00020000);
-    const __amdgpu_buffer_rsrc_t bsrc =
-        __builtin_amdgcn_make_buffer_rsrc((void*)bimg, 0, (int)(2 * dd * 2), 0x00020000);
-    float sx[PP_U];
-    int xo[PP_U], bo[PP_U];
-#pragma unroll
-    for (int u = 0; u < PP_U; ++u) {
-        const int rr = xr0 + 64 * u;
-        sx[u] = rr < nrows ? rs[r0 + rr] : 0.0f;
-        xo[u] = (rr * d + xk) * 4;
-        const int gc = c0 + bc0 + 128 * (u & 1);
-        bo[u] = gc < d ? (int)(((u >> 1) * dd + (int64_t)gc * d + bk) * 2) : (int)0x80000000u;
-    }
-    u32x4v xv[2][PP_U], bv[2][PP_U];
-    auto gload = [&](int set, int k0) __attribute__((always_inline)) {
-        // the step's k0 rides in soffset (SALU); lanes whose dims pass d read past the range
-        const bool xin = k0 + xk < d, bin = k0 + bk < d;
-#pragma unroll
-        for (int u = 0; u < PP_U; ++u) {
-            xv[set][u] = __builtin_amdgcn_raw_buffer_load_b128(xsrc, xin ? xo[u] : (int)0x80000000u, k0 * 4, 0);
-            bv[set][u] = __builtin_amdgcn_raw_buffer_load_b128(bsrc, bin ? bo[u] : (int)0x80000000u, k0 * 2, 0);
-        }
-    };
-    auto sstore = [&](int set, unsigned char* buf) __attribute__((always_inline)) {
-#pragma unroll
-        for (int u = 0; u < PP_U; ++u) {
-            const u32x4v v = xv[set][u];
-            uint32_t h0, l0, h1, l1;
-            split_pair(__uint_as_float(v[0]), __uint_as_float(v[1]), sx[u], h0, l0);
-            split_pair(__uint_as_float(v[2]), __uint_as_float(v[3]), sx[u], h1, l1);
-            const int off = (xr0 + 64 * u) * PP_PITCH + 2 * xk;
-            *reinterpret_cast<uint2*>(buf + off) = make_uint2(h0, h1);
-            *reinterpret_cast<uint2*>(buf + PP_PL + off) = make_uint2(l0, l1);
-            *reinterpret_cast<u32x4v*>(buf + (2 + (u >> 1)) * PP_PL + (bc0 + 128 * (u & 1)) * PP_PITCH + 2 * bk) =
-                bv[set][u];
-        }
-    };
-
-    floatx16 acc[4][4];
-#pragma unroll
-    for (int a = 0; a < 4; ++a)
-#pragma unroll
-        for (int b = 0; b < 4; ++b)
-#pragma unroll
-            for (int e = 0; e < 16; ++e) acc[a][b][e] = 0.0f;
-
-    const int fr = l & 31, fk = 16 * (l >> 5);
-    // the 48 MFMAs of one K step from stage buffer `cur`: the A fragments (x hi / lo of the
-    // wave's 4 row blocks) stay live, the B fragments are read per column block
-    auto mfma_step = [&](const unsigned char* cur) __attribute__((always_inline)) {
-        half8 ah[4], al[4];
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-            const int ar = (wr * 128 + i * 32 + fr) * PP_PITCH + fk;
-            ah[i] = *reinterpret_cast<const half8*>(cur + ar);
-            al[i] = *reinterpret_cast<const half8*>(cur + PP_PL + ar);
-        }
-#pragma unroll
-        for (int b = 0; b < 4; ++b) {
-            const int bc = (wc * 128 + b * 32 + fr) * PP_PITCH + fk;
-            const half8 bh = *reinterpret_cast<const half8*>(cur + 2 * PP_PL + bc);
-            const half8 bl = *reinterpret_cast<const half8*>(cur + 3 * PP_PL + bc);
-            // small terms first; the three MFMAs of one accumulator four apart
-#pragma unroll
-            for (int a = 0; a < 4; ++a) acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x16_f16(al[a], bh, acc[a][b], 0, 0, 0);
-#pragma unroll
-            for (int a = 0; a < 4; ++a) acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[a], bl, acc[a][b], 0, 0, 0);
-#pragma unroll
-            for (int a = 0; a < 4; ++a) acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[a], bh, acc[a][b], 0, 0, 0);
-        }
-    };
-    auto barrier = []() __attribute__((always_inline)) {
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-        __builtin_amdgcn_s_barrier();
-        asm volatile("" ::: "memory");
-    };
-    // one K step: MFMAs of stage s (buffer s & 1) with the store of stage s + 1 (register set
-    // (s + 1) & 1 -> buffer (s + 1) & 1) between them; the loads of stage s + 2 into set s & 1
-    // (stored one step ago) go out first
-    auto step = [&](int s, int set, bool load2, bool store1) __attribute__((always_inline)) {
-        unsigned char* cur = set ? st1 : st0;
-        unsigned char* nxt = set ? st0 : st1;
-        if (load2) gload(set, (s + 2) * PP_K);
-        __builtin_amdgcn_sched_barrier(0);  // the loads go out first, whatever the scheduler prefers
-        mfma_step(cur);
-        if (store1) sstore(set ^ 1, nxt);
-        // the A fragments first, then per 4 MFMAs: a B fragment read, 6 split ops, 1 LDS store
-        __builtin_amdgcn_sched_group_barrier(0x100, 8, 0);
-#pragma unroll
-        for (int i = 0; i < 12; ++i) {
-            __builtin_amdgcn_sched_group_barrier(0x8, 4, 0);
-            __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
-            __builtin_amdgcn_sched_group_barrier(0x2, 6, 0);
-            __builtin_amdgcn_sched_group_barrier(0x200, 1, 0);
-        }
-        __builtin_amdgcn_sched_barrier(0);
-        barrier();
-    };
-
-    const int nsteps = (d + PP_K - 1) / PP_K;
-    gload(0, 0);
-    if (nsteps > 1) gload(1, PP_K);
-    sstore(0, st0);
-    barrier();
-    int s = 0;
-    for (; s + 3 < nsteps; s += 2) {  // steady state: both sets in use, no conditions
-        step(s, 0, true, true);
-        step(s + 1, 1, true, true);
-    }
-    // tail (s even here, at most three steps left): constant register sets, no dynamic indexing
-    if (s < nsteps) step(s, 0, s + 2 < nsteps, s + 1 < nsteps);
-    if (s + 1 < nsteps) step(s + 1, 1, s + 3 < nsteps, s + 2 < nsteps);
-    if (s + 2 < nsteps) step(s + 2, 0, false, s + 3 < nsteps);
-    // epilogue: each wave's 16 KiB slice, waves 0-1 in stage 0's buffer, 2-3 in stage 1's (every
-    // wave passed the last barrier, so both buffers are dead)
-    store_tile<4, 4>(acc, w < 2 ? st0 : st1, w & 1, l, r0 + wr * 128, c0 + wc * 128, n, d, rs, hdr[1], y);
 }
 
 // ------------------------------------------------------------ Procrustes Gram matrix (training)
@@ -761,15 +536,6 @@ int launch_split(const float* x, int64_t n, int d, const float* rs, const _Float
     return check_launch("opq_split_gemm");
 }
 
-int launch_pp(const float* x, int64_t n, int d, const float* rs, const _Float16* bimg, const float* hdr, float* y,
-              hipStream_t st) {
-    const int64_t ct = ceil_div(d, PP_T), tiles = ceil_div(n, PP_T) * ct;
-    MIVQ_REQUIRE(tiles < ((int64_t)1 << 31), MIVQ_ERR_UNSUPPORTED, "opq_rotate_prepared: n=%lld too large for one call",
-                 (long long)n);
-    hipLaunchKernelGGL(opq_pp_gemm_kernel, dim3((unsigned)tiles), dim3(PP_NT), 0, st, x, n, d, rs, bimg, hdr, y, ct);
-    return check_launch("opq_pp_gemm");
-}
-
 size_t prep_bytes(int32_t d) { return 256 + (size_t)2 * d * d * sizeof(_Float16); }
 
 }  // namespace
@@ -827,8 +593,8 @@ extern "C" int mivq_opq_rotate_prepared(const float* x, int64_t n, int32_t d, co
                  workspace_bytes, need);
     MIVQ_REQUIRE(reinterpret_cast<uintptr_t>(workspace) % 16 == 0, MIVQ_ERR_INVALID,
                  "opq_rotate_prepared: workspace must be 16-byte aligned");
-    // the split GEMM's buffer offsets are 32-bit (MIVQ_OPQ_BUF): the B image is 4 d^2 bytes
-    MIVQ_REQUIRE(!MIVQ_OPQ_BUF || (int64_t)4 * d * d < ((int64_t)1 << 31), MIVQ_ERR_UNSUPPORTED,
+    // the split GEMM's buffer offsets are 32-bit: the B image is 4 d^2 bytes
+    MIVQ_REQUIRE((int64_t)4 * d * d < ((int64_t)1 << 31), MIVQ_ERR_UNSUPPORTED,
                  "opq_rotate_prepared: d=%d too large", d);
     hipStream_t st = as_stream(stream);
     float* rs = static_cast<float*>(workspace);
@@ -844,18 +610,8 @@ extern "C" int mivq_opq_rotate_prepared(const float* x, int64_t n, int32_t d, co
         if (rc) return rc;
         // 256 x 256 tiles (512 threads, 160 KiB) wherever a row block spans at least one such
         // tile; the 128 x 128 kernel for narrow matrices
-#ifndef MIVQ_OPQ_TILE4
-#define MIVQ_OPQ_TILE4 0
-#endif
-#ifndef MIVQ_OPQ_PP  // the round-4 4-wave pipelined kernel: measured slower (17.4 vs 16.2 ms), not the default
-#define MIVQ_OPQ_PP 0
-#endif
-        // (the pipelined kernel's buffer offsets into the B image are 32-bit: 4 d^2 < 2^31)
-        if (d >= 256 && cn >= 256 && MIVQ_OPQ_PP && (int64_t)4 * d * d < ((int64_t)1 << 31))
-            rc = launch_pp(xc, cn, d, rs + c0, bimg, hdr, yc, st);
-        else if (d >= 256 && cn >= 256)
-            rc = MIVQ_OPQ_TILE4 ? launch_split<TileW, 2, 2, 4, 4>(xc, cn, d, rs + c0, bimg, hdr, yc, st)
-                                : launch_split<TileL, 4, 2, 2, 4>(xc, cn, d, rs + c0, bimg, hdr, yc, st);
+        if (d >= 256 && cn >= 256)
+            rc = launch_split<TileL, 4, 2, 2, 4>(xc, cn, d, rs + c0, bimg, hdr, yc, st);
         else
             rc = launch_split<TileS, 2, 2, 2, 2>(xc, cn, d, rs + c0, bimg, hdr, yc, st);
         if (rc) return rc;

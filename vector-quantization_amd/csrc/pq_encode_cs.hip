@@ -60,19 +60,15 @@ constexpr int kGcListNc = 4;  // wide-subspace resolve: pieces of a centroid row
 constexpr int kWideWaves = 4;
 constexpr int cs_waves(int KS) { return KS <= 6 ? kWaves : kWideWaves; }
 constexpr int kRsrcWord3 = 0x00020000;  // gfx9 buffer resource: 32-bit data format
-constexpr int kXAux = 2;  // x stream cache policy: nt (read once; round 4 measured the others)
-#ifndef MIVQ_AB_XAUX48  // A/B builds (tools/build_ab.sh): the dsub-48 filter's policy
-#define MIVQ_AB_XAUX48 2
-#endif
-constexpr int kXAux48 = MIVQ_AB_XAUX48;
-#ifndef MIVQ_AB_DIRECT  // A/B builds: 1 = codes stored in the (n, M) output layout directly (no transpose launch)
-#define MIVQ_AB_DIRECT 0
-#endif
-constexpr bool kDirect = MIVQ_AB_DIRECT != 0;
-// Byte of (row, subspace m) in the code buffer: (M, n) scratch (then transposed), or the (n, M)
-// output itself (kDirect).
+// x stream cache policy: nt (read once).  Rounds 4-5 measured the others, also for the dsub-48
+// filter alone (whose odd subspaces share a cache line with their neighbour): no gain.
+constexpr int kXAux = 2;
+// Byte of (row, subspace m) in the (M, n) code scratch (transposed once at the end).  Round 5
+// measured the codes stored in the (n, M) output directly (1-B stores 16 B apart, no transpose
+// launch): no faster per call.
 __device__ __forceinline__ int64_t code_at(int64_t row, int m, int64_t n, int M) {
-    return kDirect ? row * M + m : (int64_t)m * n + row;
+    (void)M;
+    return (int64_t)m * n + row;
 }
 
 // Keeps the three largest of a stream of packed scores.  Inline asm because the compiler
@@ -316,7 +312,7 @@ __global__ __launch_bounds__(NW * 64) void pq_encode_cs_kernel(
                 // the block's uniform offset goes in soffset (SALU; gfx950 range-checks
                 // voffset + soffset, tools/probes/soffset_range.hip), the lane's in voffset
                 const int so = (vb * 32 + ibase(i)) * XS * 4 + hh * (16 * KT * 4);
-                const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(xr_rsrc, voff[i % PER], so, DS == 48 ? kXAux48 : kXAux);
+                const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(xr_rsrc, voff[i % PER], so, kXAux);
                 dst[i] = make_float4(__uint_as_float(v[0]), __uint_as_float(v[1]), __uint_as_float(v[2]),
                                      __uint_as_float(v[3]));
             }
@@ -1028,82 +1024,28 @@ __global__ __launch_bounds__(kMWaves * 64) __attribute__((amdgpu_waves_per_eu(1,
     // Full batches first (claimed from ctr[0]; their A operands take 192 registers, so their
     // gathers are not prefetched), then pair batches (claimed from ctr[1]) with the next pair
     // batch's gather in flight while the current one is computed.
-#ifndef MIVQ_AB_RES  // A/B builds: 1 = the A operands loaded once per wave, 2 = and the next full batch's gather in flight
-#define MIVQ_AB_RES 0
-#endif
-    if constexpr (MIVQ_AB_RES == 0 || GC) {
+    // (Round 5 measured the A operands loaded once per wave, with and without the next full
+    // batch's gather in flight: no faster)
     for (;;) {
-            int b = 0;
-            if (l == 0) b = atomicAdd(&ctr[0], 1);
-            b = __builtin_amdgcn_readfirstlane(__shfl(b, 0));
-            if (b >= nbf) break;
-            uint2 it;
-            int cntb;
-            batch_info(b, it, cntb);
-            f32x4 v[NL];
-            gather_issue(cntb, (int)it.x, v);
-            half8 aa[GC ? 1 : 8][KS];
-            if constexpr (!GC) {
+        int bb = 0;
+        if (l == 0) bb = atomicAdd(&ctr[0], 1);
+        bb = __builtin_amdgcn_readfirstlane(__shfl(bb, 0));
+        if (bb >= nbf) break;
+        uint2 it;
+        int cntb;
+        batch_info(bb, it, cntb);
+        f32x4 v[NL];
+        gather_issue(cntb, (int)it.x, v);
+        half8 aa[GC ? 1 : 8][KS];
+        if constexpr (!GC) {
 #pragma unroll
-                for (int cb = 0; cb < 8; ++cb)
+            for (int cb = 0; cb < 8; ++cb)
 #pragma unroll
-                    for (int ks = 0; ks < KS; ++ks) aa[cb][ks] = im[(cb * KS + ks) * 64 + l];
-            }
-            gather_commit(v);
-            full_batch(aa, cntb, (int)it.x);
-            lds_fence();  // the tile is rewritten by the next commit
+                for (int ks = 0; ks < KS; ++ks) aa[cb][ks] = im[(cb * KS + ks) * 64 + l];
         }
-    } else if (nbf > 0) {
-        half8 aa[8][KS];
-#pragma unroll
-        for (int cb = 0; cb < 8; ++cb)
-#pragma unroll
-            for (int ks = 0; ks < KS; ++ks) aa[cb][ks] = im[(cb * KS + ks) * 64 + l];
-        auto claim_full = [&]() __attribute__((always_inline)) {
-            int bb = 0;
-            if (l == 0) bb = atomicAdd(&ctr[0], 1);
-            return __builtin_amdgcn_readfirstlane(__shfl(bb, 0));
-        };
-        if constexpr (MIVQ_AB_RES == 1) {
-            for (;;) {
-                const int b = claim_full();
-                if (b >= nbf) break;
-                uint2 it;
-                int cntb;
-                batch_info(b, it, cntb);
-                f32x4 v[NL];
-                gather_issue(cntb, (int)it.x, v);
-                gather_commit(v);
-                full_batch(aa, cntb, (int)it.x);
-                lds_fence();
-            }
-        } else {
-            int fb = claim_full();
-            uint2 fit = make_uint2(0u, 0u);
-            int fcnt = 0;
-            f32x4 fa[NL], fb2[NL];
-            if (fb < nbf) batch_info(fb, fit, fcnt);
-            gather_issue(fb < nbf ? fcnt : 0, (int)fit.x, fa);
-            auto fiter = [&](const f32x4 (&vc)[NL], f32x4 (&vn)[NL]) __attribute__((always_inline)) {
-                const int bn = claim_full();
-                uint2 itn = make_uint2(0u, 0u);
-                int cntn = 0;
-                if (bn < nbf) batch_info(bn, itn, cntn);
-                __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
-                gather_commit(vc);
-                gather_issue(cntn, (int)itn.x, vn);
-                full_batch(aa, fcnt, (int)fit.x);
-                lds_fence();
-                fb = bn;
-                fit = itn;
-                fcnt = cntn;
-            };
-            while (fb < nbf) {
-                fiter(fa, fb2);
-                if (fb >= nbf) break;
-                fiter(fb2, fa);
-            }
-        }
+        gather_commit(v);
+        full_batch(aa, cntb, (int)it.x);
+        lds_fence();  // the tile is rewritten by the next commit
     }
     // pair batches: the first one per wave is static (b = w), the rest are claimed from ctr[1]
     int b = w, cntb = 0;
@@ -1315,7 +1257,7 @@ hipError_t launch_pq_encode_cs(int KS, const float* x, int64_t n, int d, int M, 
     switch (KS) {
 #define MIVQ_CS_CASE(k)                                                                                        \
     case k:                                                                                                    \
-        e = launch_pq_encode_cs_v<k>(x, n, d, M, dsub, C, cn, img, hinit, bnd, pd, bnd2, kDirect ? codes : codesT, \
+        e = launch_pq_encode_cs_v<k>(x, n, d, M, dsub, C, cn, img, hinit, bnd, pd, bnd2, codesT,            \
                                      items, counts, st);                                                       \
         break;
         MIVQ_CS_CASE(1) MIVQ_CS_CASE(2) MIVQ_CS_CASE(3) MIVQ_CS_CASE(4) MIVQ_CS_CASE(5) MIVQ_CS_CASE(6)
@@ -1324,7 +1266,6 @@ hipError_t launch_pq_encode_cs(int KS, const float* x, int64_t n, int d, int M, 
         default: return hipErrorInvalidValue;
     }
     if (e != hipSuccess) return e;
-    if (kDirect) return hipSuccess;  // the kernels wrote the (n, M) layout
     const bool v16 = n % 16 == 0 && (reinterpret_cast<uintptr_t>(codesT) % 16) == 0 &&
                      (reinterpret_cast<uintptr_t>(codes) % 16) == 0 && M <= 256;
     if (v16 && M == 16)

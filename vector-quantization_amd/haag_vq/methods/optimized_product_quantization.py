@@ -87,7 +87,7 @@ def _mm(a: torch.Tensor, b: torch.Tensor) -> torch.Tensor:
     return _native.extrabitq_rotate(a.contiguous(), b.contiguous(), False)
 
 
-def polar_factor(G: torch.Tensor, tol: float = 1e-13, max_iter: int = 60) -> torch.Tensor:
+def polar_factor(G: torch.Tensor, tol: float = 1e-13, max_iter: int = 60, info: dict | None = None) -> torch.Tensor:
     """The orthogonal polar factor Q = U V^T of a square fp64 matrix G = U S V^T (what
     faiss OPQMatrix::train takes from its SVD), by the Newton-Schulz iteration
     Q <- Q (3 I - Q^T Q) / 2 on the fp64 MFMA GEMM (erq_rotate_kernel) instead of rocsolver's
@@ -98,23 +98,33 @@ def polar_factor(G: torch.Tensor, tol: float = 1e-13, max_iter: int = 60) -> tor
     vector -- cannot rule that out).  It doubles the digits once every singular value is near 1,
     and stops at ||Q^T Q - I||_F < tol sqrt(d) or once that error stalls at the fp64 rounding
     floor of the GEMMs.  A G the iteration cannot orthogonalise (rank deficient, or not
-    converged within max_iter: condition numbers far beyond 1e8) falls back to the SVD."""
+    converged within max_iter: condition numbers far beyond 1e8) falls back to the SVD; a
+    rank-deficient G is recognised by its error stalling above 1e-8 (the zero singular values
+    stay at zero, ||Q^T Q - I|| levels off at sqrt(#zeros)) for 4 steps, not after max_iter.
+    ``info`` (optional dict) receives {"path": "newton-schulz" | "svd", "iters": steps}."""
     d = G.shape[0]
     I = torch.eye(d, dtype=torch.float64, device=G.device)
     GtG = _mm(G.T, G)
     bound = min(float(G.norm()), float(GtG.abs().sum(dim=1).max()) ** 0.5)
     if bound > 0.0 and bound < float("inf"):
         Q = G / bound
-        prev = float("inf")
-        for _ in range(max_iter):
+        prev, stall = float("inf"), 0
+        for it in range(max_iter):
             T = _mm(Q.T, Q)
             err = float((T - I).norm())
             if err < tol * d ** 0.5 or (err < 1e-8 and err > 0.25 * prev):
+                if info is not None:
+                    info.update(path="newton-schulz", iters=it)
                 return Q  # converged (quadratic phase stalled: the rounding floor)
             if not err < 1e3:  # non-finite
                 break
+            stall = stall + 1 if err >= 0.999 * prev else 0
+            if stall >= 4:
+                break  # levelled off above 1e-8: zero singular values
             prev = err
             Q = 1.5 * Q - 0.5 * _mm(Q, T)
+    if info is not None:
+        info.update(path="svd", iters=it + 1 if bound > 0.0 and bound < float("inf") else 0)
     U, _, Vh = torch.linalg.svd(G)
     return U @ Vh
 

@@ -1,6 +1,6 @@
 #!/bin/bash
 # round-5 session 1: slice pipeline (filter on two streams, resolve on a high-priority stream)
-cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../..}"
 bash tools/gpu_session.sh \
   "python -u -m pytest tests/test_kernels_gpu.py -m gpu -q -x -k 'pq_encode' --timeout 120 --timeout-method thread" \
   "python -u tools/probe_pipe.py --n 1000000 --cfg base:PIPE=0 --cfg s2:SLICES=2 --cfg s3:SLICES=3 --cfg s4:SLICES=4 --cfg s8:SLICES=8" \

@@ -1,6 +1,6 @@
 #!/bin/bash
 # round-5 session 10: certification rate and time of the filtered ADC vs the integer grid span
-cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../..}"
 bash tools/gpu_session.sh \
   "MIVQ_ADC_STATS=1 python -u tools/probe_adc.py --reps 3 2>&1 | sort | uniq -c | sort -rn | head -20" \
   "MIVQ_LIB=$PWD/vector-quantization_amd/lib/ab/libmivq_span1.0.so MIVQ_ADC_STATS=1 python -u tools/probe_adc.py --reps 3 2>&1 | sort | uniq -c | sort -rn | head -20" \

@@ -1,6 +1,6 @@
 #!/bin/bash
 # round-5 session 11: per-lane top-3 (certification rate, time) and entry widths 8 / 7 / 6 bits
-cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../..}"
 AB=$PWD/vector-quantization_amd/lib/ab
 stats() { python -u tools/probe_adc.py --reps 3 "$@" 2>&1 | sort | uniq -c | sort -rn | head -8; }
 bash tools/gpu_session.sh \

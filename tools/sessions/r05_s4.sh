@@ -1,7 +1,7 @@
 #!/bin/bash
 # round-5 session 4: filtered ADC (tests + timing), the pruned encode file (bit-exact tests and
 # interleaved A/Bs: pre-prune build, resolve A operands per wave, direct (n, M) code stores)
-cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../..}"
 bash tools/gpu_session.sh \
   "python -u -m pytest tests/test_adc_filtered_gpu.py tests/test_kernels_gpu.py -m gpu -q -x -rf --timeout 300 --timeout-method thread" \
   "python -u tools/probe_adc.py" \

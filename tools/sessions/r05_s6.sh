@@ -1,6 +1,6 @@
 #!/bin/bash
 # round-5 session 6: filtered ADC tests (NaN hook), u8-entry table A/B, then session 5's items
-cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../..}"
 bash tools/gpu_session.sh \
   "python -u -m pytest tests/test_adc_filtered_gpu.py -m gpu -q -x -rf --timeout 300 --timeout-method thread" \
   "MIVQ_LIB=$PWD/vector-quantization_amd/lib/ab/libmivq_adce8.so python -u -m pytest tests/test_adc_filtered_gpu.py -m gpu -q -x -rf --timeout 300 --timeout-method thread" \

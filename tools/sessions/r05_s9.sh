@@ -1,7 +1,7 @@
 #!/bin/bash
 # round-5 session 9: kernel trace of the filtered ADC (where the 1M x 1000 call's time goes) and
 # the sharded-index test
-cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../..}"
 mkdir -p gpurun_out
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/adcprof -o run --output-format csv -- python -u tools/probe_adc.py --reps 4 > gpurun_out/adcprof.log 2>&1
 rc=$?; echo "rocprof exit $rc"; [ $rc -ne 0 ] && exit $rc

@@ -113,7 +113,10 @@ def _free_port() -> int:
 def launch_ranks(a) -> int:
     """One process per GPU under torch.distributed.run, started as a child (never exec'd)."""
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={a.gpus}",
-           "--master-addr=127.0.0.1", f"--master-port={_free_port()}", str(Path(__file__).resolve())] + sys.argv[1:]
+           "--master-addr=127.0.0.1", f"--master-port={_free_port()}",
+           # "--": torchrun's parser would take bench flags that abbreviate its own options
+           # (--n, --d) as ambiguous options of its own
+           "--", str(Path(__file__).resolve())] + sys.argv[1:]
     env = dict(os.environ)
     env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
     env.setdefault("OMP_NUM_THREADS", "1")
@@ -208,7 +211,7 @@ def timed(fn, steps, warmup, world=1, dev=None, settle_ms=0.0):
     torch.cuda.synchronize()
     dt = time.perf_counter() - t0
     if world > 1:
-        t = torch.tensor([dt], device=dev, dtype=torch.float64)
+        t = torch.tensor([dt], device=dev if dist.get_backend() == "nccl" else "cpu", dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         dt = float(t.item())
     return dt / steps, float(np.mean([s.elapsed_time(e) for s, e in evs]))
@@ -722,8 +725,14 @@ def main():
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world > 1:
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        # one process per GPU; VQ_DIST_BACKEND=gloo rehearses the same ranks sharing a GPU
+        # (host-staged collectives, tests/test_sharded_gpu.py) -- RCCL otherwise
+        gpu = local % max(1, torch.cuda.device_count())
+        torch.cuda.set_device(gpu)
+        if os.environ.get("VQ_DIST_BACKEND", "nccl") == "gloo":
+            dist.init_process_group("gloo")
+        else:
+            dist.init_process_group("nccl", device_id=torch.device("cuda", gpu))
     dev = _native.require_device()
     head_only = rank == 0 and world == 1
 

@@ -39,3 +39,10 @@ def test_gpus_must_match_world_size():
                        text=True, timeout=120, env=env, cwd=str(ROOT))
     assert p.returncode != 0
     assert "WORLD_SIZE" in p.stderr
+
+
+def test_launcher_passes_flags_that_abbreviate_torchrun_options():
+    """--n / --d abbreviate several torch.distributed.run options (--nnodes, --nproc-per-node,
+    --duplicate-*): the launcher ends torchrun's options with "--" so they reach bench.py."""
+    out = _run("--gpus", "2", "--dry-run", "--n", "1000", "--d", "64", "--nq", "10")
+    assert out["n_gpus"] == 2 and out["merged_equals_single"] is True

@@ -48,7 +48,7 @@ def test_rank_command_uses_loopback_and_module():
     cmd = rank_command(4, ["streaming-sweep", "--gpus", "4"], port=12345)
     assert cmd[1:3] == ["-m", "torch.distributed.run"]
     assert "--nproc-per-node=4" in cmd and "--master-addr=127.0.0.1" in cmd and "--master-port=12345" in cmd
-    assert cmd[-5:] == ["-m", "haag_vq", "streaming-sweep", "--gpus", "4"]
+    assert cmd[-6:] == ["-m", "--", "haag_vq", "streaming-sweep", "--gpus", "4"]
 
 
 @pytest.mark.parametrize("gpus", [2, 3])

@@ -119,3 +119,24 @@ def test_sweep_two_ranks_deal_configs(dev, tmp_path):
         assert two[M]["n_gpus"] == 2 and one[M]["n_gpus"] == 1
         assert two[M]["reconstruction_distortion"] == one[M]["reconstruction_distortion"]
         assert two[M]["compression_ratio"] == one[M]["compression_ratio"]
+
+
+@pytest.mark.gpu
+def test_bench_two_ranks_one_gpu(dev, tmp_path):
+    """`bench.py --gpus 2` end to end on one card (VQ_DIST_BACKEND=gloo: host-staged
+    collectives instead of RCCL): the launcher, per-rank shards, the codebook and query
+    broadcasts, max-over-ranks timing, the top-k exchange and merge, config #5 -- the code the
+    driver's multi-GPU runs execute, with small shapes.  The sharded ADC lists must agree with
+    the sharded decode + exact ranking of the same codes (near-ties aside)."""
+    cmd = [sys.executable, "-u", str(ROOT / "bench.py"), "--gpus", "2", "--n", "100000", "--steps", "2",
+           "--warmup", "1", "--nq", "64", "--gt-queries", "32", "--no-cpu-baseline", "--no-alt-data",
+           "--no-north-star", "--no-configs", "--config5-rows", "60000", "--config5-nq", "64"]
+    p = subprocess.run(cmd, capture_output=True, text=True, env=_env(), timeout=600, cwd=str(tmp_path))
+    assert p.returncode == 0, p.stdout[-3000:] + p.stderr[-3000:]
+    lines = [ln for ln in p.stdout.splitlines() if ln.startswith("{") and '"metric"' in ln]
+    assert len(lines) == 1, p.stdout[-3000:]
+    out = json.loads(lines[0])
+    assert out["n_gpus"] == 2 and out["value"] > 0 and out["config"]["parallelism"] == "row-sharded x2"
+    assert out["adc"]["n_total"] == 200000 and out["adc"]["topk_agreement_adc_vs_decode_exact"] >= 0.99
+    c5 = out["config5"]
+    assert c5["n_gpus"] == 2 and c5["rows_total"] == 120000 and c5["adc"]["topk_agreement_adc_vs_decode_exact"] >= 0.99

@@ -47,7 +47,10 @@ def free_port() -> int:
 def rank_command(gpus: int, module_args: List[str], port: Optional[int] = None) -> List[str]:
     """The child command line: torch.distributed.run over 127.0.0.1 running ``python -m haag_vq``."""
     return [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={int(gpus)}",
-            "--master-addr=127.0.0.1", f"--master-port={port or free_port()}", "-m", "haag_vq"] + list(module_args)
+            "--master-addr=127.0.0.1", f"--master-port={port or free_port()}",
+            # "--" ends torchrun's options: flags of ours that abbreviate one of its options
+            # (e.g. --n, --d) would otherwise be rejected as ambiguous
+            "-m", "--", "haag_vq"] + list(module_args)
 
 
 def launch_ranks(gpus: int, module_args: List[str], extra_env: Optional[dict] = None) -> int:

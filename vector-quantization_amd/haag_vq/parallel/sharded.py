@@ -49,8 +49,14 @@ def _world() -> Tuple[int, int]:
 
 
 def broadcast_(t: torch.Tensor, src: int = 0) -> torch.Tensor:
+    """In-place broadcast from ``src``; under gloo a device tensor goes through a host copy."""
     if _world()[1] > 1:
-        dist.broadcast(t, src=src)
+        if _host_collectives() and t.device.type != "cpu":
+            h = t.cpu()
+            dist.broadcast(h, src=src)
+            t.copy_(h)
+        else:
+            dist.broadcast(t, src=src)
     return t
 
 

@@ -1199,6 +1199,8 @@ hipError_t launch_pq_encode_cs_v(const float* x, int64_t n, int d, int M, int ds
     }
     if constexpr (KS == 4) {  // D = 1024, M = 16 (BASELINE config #5)
         if (dsub == 64) {
+            // (round 5: 12 waves with two pipelined accumulators, 12 with one and 8 waves measured
+            // 0.5-4 % slower, profiles/r05_s20)
             constexpr int NW64 = 16;
             kern = pq_encode_cs_kernel<4, 1, 64, NW64>;
             nw_launch = NW64;

@@ -501,7 +501,10 @@ struct AdcQStat {
 // u16 entries: 6 bits lets four lookups share one unpack, and certified as many queries once the
 // grid span followed the mean offset); lanes keep 3 keys per query (2 left ~2 % of the queries
 // uncertified on Gaussian rows, 3 none).
-constexpr int kAdcBits = 6;
+#ifndef MIVQ_AB_ADC_BITS  // A/B builds: bits per table entry (6: four lookups per unpack, 5: eight)
+#define MIVQ_AB_ADC_BITS 6
+#endif
+constexpr int kAdcBits = MIVQ_AB_ADC_BITS;
 constexpr int kLaneKeys = 3;
 constexpr double kAdcSpan = 2.0;  // the grid's span in mean offsets above the minimum
 __host__ __device__ constexpr int adc_qmax(int) { return (1 << kAdcBits) - 1; }
@@ -664,7 +667,6 @@ __global__ __launch_bounds__(kScanWaves * 64) void adc_qscan_kernel(
 
     const int64_t rbeg = (int64_t)blockIdx.x * chunk_rows;
     const int64_t rend = min(n, rbeg + chunk_rows);
-    const uint32_t tbase = (uint32_t)(uintptr_t)qt;
     uint4 cw[MC];
     auto fetch = [&](int64_t row) __attribute__((always_inline)) {
         const uint4* cr = reinterpret_cast<const uint4*>(codes + row * (16 * MC));
@@ -674,7 +676,7 @@ __global__ __launch_bounds__(kScanWaves * 64) void adc_qscan_kernel(
     // entries of kAdcBits < 8 bits: 2^(8 - bits) lookups add up in the bytes themselves (no carry
     // crosses a byte) before one unpack to the u16 pairs
     constexpr int UNP = 1 << (8 - kAdcBits);
-    static_assert(UNP == 1 || UNP == 2 || UNP == 4, "entry bits");
+    static_assert(UNP == 1 || UNP == 2 || UNP == 4 || UNP == 8, "entry bits");
     const int64_t first = rbeg + (int64_t)wv * 64;
     fetch(first + lane);
     uint32_t step = 0;
@@ -696,21 +698,30 @@ __global__ __launch_bounds__(kScanWaves * 64) void adc_qscan_kernel(
         // unrolled over the code words (round 5: 0.560 -> 0.531 ms per 1000 x 1M at M = 16,
         // profiles/r05_s20): word jw is wq[jw] and its subspaces' table offset rides in the
         // ds_read immediate, instead of a register shift of wq and an address add per word
+        uint32_t a8[4] = {0u, 0u, 0u, 0u};  // byte sums of up to UNP lookups (across words)
 #pragma unroll
         for (int jw = 0; jw < 4 * MC; ++jw) {
             const uint32_t wrd = wq[jw];
             const int jofs = jw * 4 * 256;  // in 16-B entries
-            uint32_t a8[4] = {0u, 0u, 0u, 0u};  // byte sums of up to UNP lookups
 #pragma unroll
             for (int b = 0; b < 4; ++b) {
-                uint32_t cb, o1;
-                asm("v_bfe_u32 %0, %1, %2, 8" : "=v"(cb) : "v"(wrd), "i"(8 * b));
-                asm("v_lshl_add_u32 %0, %1, 4, %2" : "=v"(o1) : "v"(cb), "v"(tbase));
+                // code byte b << 4 in ONE op (SDWA byte select on the shifted operand), used as
+                // the LDS address itself: qt is this kernel's only LDS, so the dynamic segment
+                // starts at address 0 (the generic->LDS cast of qt compiles to a select of 0, 0)
+                uint32_t o1;
+                if (b == 0)
+                    asm("v_lshlrev_b32_sdwa %0, 4, %1 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:BYTE_0" : "=v"(o1) : "v"(wrd));
+                else if (b == 1)
+                    asm("v_lshlrev_b32_sdwa %0, 4, %1 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:BYTE_1" : "=v"(o1) : "v"(wrd));
+                else if (b == 2)
+                    asm("v_lshlrev_b32_sdwa %0, 4, %1 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:BYTE_2" : "=v"(o1) : "v"(wrd));
+                else
+                    asm("v_lshlrev_b32_sdwa %0, 4, %1 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:BYTE_3" : "=v"(o1) : "v"(wrd));
                 const u32x4v t0 = *(reinterpret_cast<const lds_u4*>((uintptr_t)o1) + jofs + b * 256);
                 const uint32_t tv[4] = {t0.x, t0.y, t0.z, t0.w};
 #pragma unroll
-                for (int wd = 0; wd < 4; ++wd) a8[wd] = (b % UNP == 0) ? tv[wd] : a8[wd] + tv[wd];
-                if ((b + 1) % UNP == 0) {
+                for (int wd = 0; wd < 4; ++wd) a8[wd] = ((4 * jw + b) % UNP == 0) ? tv[wd] : a8[wd] + tv[wd];
+                if ((4 * jw + b + 1) % UNP == 0) {
 #pragma unroll
                     for (int wd = 0; wd < 4; ++wd) {  // bytes (4w, 4w+2, 4w+1, 4w+3) -> u16 pairs
                         acc[2 * wd] += __builtin_amdgcn_perm(a8[wd], a8[wd], 0x0C020C00u);

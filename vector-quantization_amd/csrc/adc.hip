@@ -501,10 +501,9 @@ struct AdcQStat {
 // u16 entries: 6 bits lets four lookups share one unpack, and certified as many queries once the
 // grid span followed the mean offset); lanes keep 3 keys per query (2 left ~2 % of the queries
 // uncertified on Gaussian rows, 3 none).
-#ifndef MIVQ_AB_ADC_BITS  // A/B builds: bits per table entry (6: four lookups per unpack, 5: eight)
-#define MIVQ_AB_ADC_BITS 6
-#endif
-constexpr int kAdcBits = MIVQ_AB_ADC_BITS;
+// (5 bits, eight lookups per unpack: 3-5 % faster on clustered rows and the config #5 shape, but
+// 1.6x slower on 1M x 1536 Gaussian rows, whose queries it mostly fails to certify; r05_s22)
+constexpr int kAdcBits = 6;
 constexpr int kLaneKeys = 3;
 constexpr double kAdcSpan = 2.0;  // the grid's span in mean offsets above the minimum
 __host__ __device__ constexpr int adc_qmax(int) { return (1 << kAdcBits) - 1; }

@@ -737,10 +737,12 @@ __global__ __launch_bounds__(kScanWaves * 64) void adc_qscan_kernel(
             mk[1][qq] = umed3(mk[0][qq], mk[1][qq], key);
             mk[0][qq] = min(mk[0][qq], key);
         };
+        // the row's low half once per row: each key is then one v_lshl_or / v_and_or
+        const uint32_t lo16 = step | inval;
 #pragma unroll
         for (int j = 0; j < NACC; ++j) {
-            insert(2 * j, ((acc[j] << 16) | step) | inval);                // query 2j
-            insert(2 * j + 1, ((acc[j] & 0xFFFF0000u) | step) | inval);    // query 2j + 1
+            insert(2 * j, (acc[j] << 16) | lo16);                 // query 2j
+            insert(2 * j + 1, (acc[j] & 0xFFFF0000u) | lo16);     // query 2j + 1
         }
     }
     // per query: select the candidates below T, the bound B, write K1 slots.  A lane's unlisted

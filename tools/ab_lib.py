@@ -1,6 +1,6 @@
 """Interleaved A/B of mivq_pq_encode between two builds of libmivq.so (same process, same data).
 
-usage: python tools/ab_lib.py OTHER.so [--what encode|adc] [--n 1000000] [--d 1536] [--M 16]
+usage: python tools/ab_lib.py OTHER.so [--what encode|adc|lut] [--n 1000000] [--d 1536] [--M 16]
                               [--data gaussian] [--reps 10] [--nq 1000] [--k 10]
 The in-tree library (vector-quantization_amd/lib/libmivq.so) is "this"; OTHER.so is e.g. a
 build of the previous commit (git stash; make; cp lib/libmivq.so /tmp/old.so; git stash pop).
@@ -40,7 +40,7 @@ def main():
     ap.add_argument("--M", type=int, default=16)
     ap.add_argument("--data", default="gaussian")
     ap.add_argument("--reps", type=int, default=10)
-    ap.add_argument("--what", choices=("encode", "adc"), default="encode")
+    ap.add_argument("--what", choices=("encode", "adc", "lut"), default="encode")
     ap.add_argument("--nq", type=int, default=1000)
     ap.add_argument("--k", type=int, default=10)
     a = ap.parse_args()
@@ -71,6 +71,19 @@ def main():
         run_encode(k)
     torch.cuda.synchronize()
     same = bool(torch.equal(state["this"][2], state["other"][2]))
+    if a.what == "lut":  # mivq_adc_lut alone: the LUTs of nq queries, compared bit for bit
+        Q = synth(a.nq, a.d, 7, dev, kind=a.data)
+        luts = {k: torch.empty((a.nq, a.M, 256), dtype=torch.float32, device=dev) for k in libs}
+
+        def run_lut(k):
+            rc = libs[k].mivq_adc_lut(P(Q.data_ptr()), a.nq, a.d, a.M, 8, P(C.data_ptr()), 1, P(luts[k].data_ptr()), P(st))
+            assert rc == 0, rc
+
+        run = run_lut
+        for k in libs:
+            run_lut(k)
+        torch.cuda.synchronize()
+        same = bool(torch.equal(luts["this"], luts["other"]))
     if a.what == "adc":
         codes = state["this"][2]
         Q = synth(a.nq, a.d, 7, dev, kind=a.data)

@@ -27,7 +27,9 @@ constexpr int kScanWaves = 16;  // waves per scan workgroup (adc and flat)
 // block of kLutQ queries whose sub-vectors sit in LDS (broadcast reads).  The centroid row
 // is read 4 floats at a time and every query's chain advances over those 4 dims in order,
 // so each (query, k) chain is the canonical sequential one.  Stores are coalesced along k.
-constexpr int kLutQ = 32;
+// 16 queries per workgroup (round 5: 57 -> 46 us for 1000 queries at M = 16 against 32 -- twice
+// the workgroups to spread over the CUs; 8: 50 us; profiles/r05_s24)
+constexpr int kLutQ = 16;
 
 __global__ __launch_bounds__(256) void adc_lut_kernel(const float* __restrict__ q, int64_t nq, int d, int M, int ksub,
                                                        int dsub, const float* __restrict__ C, int metric,

@@ -327,9 +327,13 @@ def adc_leg(X, C, codes, a, rank, world, dev, Q, k, gt_queries, reps=3, cpu=True
                         "achieved": lds_bytes / (scan_ms * 1e-3) / 1e9, "peak": LDS_PEAK_GBS, "unit": "GB/s",
                         "frac": lds_bytes / (scan_ms * 1e-3) / 1e9 / LDS_PEAK_GBS, "scan_ms": scan_ms,
                         "lds_bytes_per_query_row": M * 4,
+                        # the bytes the integer scan actually reads: one byte per (query, row, subspace)
+                        "lds_bytes_read_frac": nq * n * M / (scan_ms * 1e-3) / 1e9 / LDS_PEAK_GBS,
                         "note": "algorithmic bytes = one fp32 LUT entry per (query, row, subspace), the canonical "
-                                "ADC's work; the filtered scan itself reads 2-B integer entries (M * 2 B per "
-                                "(query, row) from LDS)"}}
+                                "ADC's table reads (SURVEY 8d); the filtered search (DESIGN 3.3) scans 1-B 6-bit "
+                                "entries, 16 queries per 16-B read, so frac can exceed 1; its own LDS reads are "
+                                "lds_bytes_read_frac of the peak and its scan is bound by VALU issue (177 VALU per "
+                                "row and 16 queries)"}}
     if cpu and rank == 0 and world == 1:
         O = _oracle()
         # a bounded sample: ~1 s wall on the box's 16 threads (~16 thread-s)

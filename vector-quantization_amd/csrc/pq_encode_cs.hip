@@ -1187,6 +1187,8 @@ hipError_t launch_pq_encode_cs_v(const float* x, int64_t n, int d, int M, int ds
     int nw_launch = NW, smem_launch = smem;
     // specialised shapes (addresses and load counts folded; waves per shape measured)
     if constexpr (KS == 6) {  // D = 1536, M = 16: the headline
+        // (round 5: 16 waves, one accumulator and the x / centroid fragments read per centroid
+        // block to fit 128 VGPRs: 0.3-3 % slower than these 12, profiles/r05_s26)
         if (dsub == 96) kern = pq_encode_cs_kernel<6, 3, 96, 12>;
     }
     if constexpr (KS == 3) {  // D = 1536, M = 32 (the OPQ32 / PQ32 shape of BASELINE config #3)

@@ -609,7 +609,8 @@ extern "C" int mivq_opq_rotate_prepared(const float* x, int64_t n, int32_t d, co
         int rc = check_launch("opq_row_scale");
         if (rc) return rc;
         // 256 x 256 tiles (512 threads, 160 KiB) wherever a row block spans at least one such
-        // tile; the 128 x 128 kernel for narrow matrices
+        // tile; the 128 x 128 kernel for narrow matrices (round 5: 128 x 128 everywhere, two
+        // workgroups per CU whose barriers are independent: 18.0 vs 14.6 ms, profiles/r05_s27)
         if (d >= 256 && cn >= 256)
             rc = launch_split<TileL, 4, 2, 2, 4>(xc, cn, d, rs + c0, bimg, hdr, yc, st);
         else

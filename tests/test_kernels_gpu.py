@@ -567,9 +567,10 @@ def test_rabitq_search_bit_exact(dev, oracle, nq, n, d, qb, k, metric):
 
 @pytest.mark.parametrize("d", [96, 192])
 def test_pq_encode_slice_boundary_wide_shapes(dev, oracle, d):
-    """the 2^21-row slicing at the shapes it was tuned for — dsub 96 (KS 6, the D96
-    wave count) and dsub 192 (KS 12, K-halves filter) with M = 1 — rows on both sides of the
-    boundary and the ragged last slice (1001 rows: the generic code transpose) vs the oracle."""
+    """the slicing of large calls (2^20-row slices since round 5) at the shapes it was
+    tuned for — dsub 96 (KS 6, the D96 wave count) and dsub 192 (KS 12, K-halves filter) with
+    M = 1 — rows on both sides of the boundaries and the ragged last slice (1001 rows: the
+    generic code transpose) vs the oracle."""
     from haag_vq import _native
 
     rng = np.random.default_rng(d)
@@ -579,13 +580,13 @@ def test_pq_encode_slice_boundary_wide_shapes(dev, oracle, d):
     C = _codebook(rng, X0, 1, 256)
     Cd = _t(C, dev)
     got = _h(_native.pq_encode(Xd, Cd, _native.pq_prepare(Cd, 8), 8))
-    for lo, hi in ((0, 1500), ((1 << 21) - 2500, n)):
+    for lo, hi in ((0, 1500), ((1 << 20) - 2500, (1 << 20) + 2500), ((1 << 21) - 2500, n)):
         np.testing.assert_array_equal(got[lo:hi], oracle.pq_encode(_h(Xd[lo:hi]), C))
 
 
 def test_pq_encode_slices_large_calls(dev, oracle):
-    """Calls above 2^21 rows run as 2^21-row slices: rows on both sides of the slice boundary and
-    in the ragged last slice equal the oracle (and a second slice boundary, 2^22)."""
+    """Calls above 2^20 rows run as 2^20-row slices: rows on both sides of slice boundaries
+    (2^20, 2^21, 2^22) and in the ragged last slice equal the oracle."""
     from haag_vq import _native
 
     rng = np.random.default_rng(21)
@@ -594,5 +595,6 @@ def test_pq_encode_slices_large_calls(dev, oracle):
     C = _codebook(rng, X[:4096], M, 256)
     Cd = _t(C, dev)
     got = _h(_native.pq_encode(_t(X, dev), Cd, _native.pq_prepare(Cd, 8), 8))
-    for lo, hi in ((0, 2000), ((1 << 21) - 3000, (1 << 21) + 3000), ((1 << 22) - 2000, n)):
+    for lo, hi in ((0, 2000), ((1 << 20) - 3000, (1 << 20) + 3000), ((1 << 21) - 3000, (1 << 21) + 3000),
+                   ((1 << 22) - 2000, n)):
         np.testing.assert_array_equal(got[lo:hi], oracle.pq_encode(np.ascontiguousarray(X[lo:hi]), C))

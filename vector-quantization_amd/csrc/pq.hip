@@ -838,11 +838,14 @@ extern "C" int mivq_pq_encode(const float* x, int64_t n, int32_t d, int32_t M, i
                        M <= 512 && !(flags_in & MIVQ_PQ_LEGACY_MFMA);
     const bool mfma_ok = L.mfma && aligned && L.ks <= 8 && !exact_only && mfma_smem_bytes(L.ks, M) <= 160 * 1024;
     if (cs_ok) {
-        // Calls above 2^21 rows run as consecutive 2^21-row slices on the same stream (the
-        // workspace regions are reused, stream-ordered): the same codes, and 10M x 1536 PQ16 takes
-        // 13.85 instead of 14.43 ms (tools/probe_chunked.py: a long filter-only stretch runs at a
-        // lower power-managed clock than filters interleaved with their resolve launches)
-        constexpr int64_t kSlice = (int64_t)1 << 21;
+        // Calls above 2^20 rows run as consecutive 2^20-row slices on the same stream (the
+        // workspace regions are reused, stream-ordered): the same codes, and a 10M x 1536 PQ16
+        // call runs faster than in one piece (round 3: 13.85 vs 14.43 ms at 2^21-row slices,
+        // tools/probe_chunked.py: a long filter-only stretch runs at a lower power-managed clock
+        // than filters interleaved with their resolve launches; round 5: 2^20-row slices another
+        // 1.2 % faster at 10M x 1536, equal at 6.65M x 1024, 2^19 / 2^22 no better,
+        // profiles/r05_s28, r05_s29)
+        constexpr int64_t kSlice = (int64_t)1 << 20;
         for (int64_t r0 = 0; r0 < n; r0 += kSlice) {
             const int64_t nc = std::min(kSlice, n - r0);
             const hipError_t e = launch_pq_encode_cs(L.ks, x + r0 * d, nc, d, M, L.dsub, centroids, cn, p + L.img,

@@ -708,7 +708,7 @@ __global__ __launch_bounds__(kScanWaves * 64) void adc_qscan_kernel(
             for (int b = 0; b < 4; ++b) {
                 // code byte b << 4 in ONE op (SDWA byte select on the shifted operand), used as
                 // the LDS address itself: qt is this kernel's only LDS, so the dynamic segment
-                // starts at address 0 (the generic->LDS cast of qt compiles to a select of 0, 0)
+                // starts at address 0 (guarded at the bound store below)
                 uint32_t o1;
                 if (b == 0)
                     asm("v_lshlrev_b32_sdwa %0, 4, %1 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:BYTE_0" : "=v"(o1) : "v"(wrd));
@@ -789,7 +789,10 @@ __global__ __launch_bounds__(kScanWaves * 64) void adc_qscan_kernel(
         }
         for (int e = used + lane; e < k1; e += 64) { od[e] = INFINITY; oi[e] = kNoId; }
         // B = 0xFFFF: every row of the part is listed
-        if (lane == 0) part_b[part * nq + q0 + qq] = B >= 0xFFFFu ? INFINITY : (float)B;
+        // (the lookups take the table at LDS address 0, i.e. no static LDS in this kernel; were
+        // there any, every bound reads 0 and every query goes to the fp32 re-run: slow, never wrong)
+        if (lane == 0)
+            part_b[part * nq + q0 + qq] = __builtin_amdgcn_groupstaticsize() != 0 ? 0.0f : B >= 0xFFFFu ? INFINITY : (float)B;
     }
 }
 

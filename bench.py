@@ -774,6 +774,14 @@ def main():
         pa = parity_check(Xa, Ca, ca, _oracle(), max_rows=200_000, fp64_rows=5000)[0] if not a.no_cpu_baseline else None
         alt = {"data": kind, "value": a.n / ea["wall_s"], "unit": "vectors/s", "ms_per_step": ea["wall_s"] * 1e3,
                "kernel_ms": ea["kernel_ms"], "roofline_frac": ea["achieved_gbs"] / HBM_PEAK_GBS, "parity": pa}
+        if not a.no_adc:
+            # the ADC leg on these rows too: recall@k means more on clustered rows than on
+            # isotropic ones, and the filter certifies a different share of the queries
+            aa = adc_leg(Xa, Ca, ca, a, 0, 1, dev, Xa[:a.nq].clone(), a.k, a.gt_queries, cpu=False)
+            alt["adc"] = {key: aa[key] for key in ("qps", "nq", "k", f"recall@{a.k}", f"recall@{a.k}_decode_exact",
+                                                   "topk_agreement_adc_vs_decode_exact", "ms_per_batch")}
+            alt["adc"]["scan_ms"] = aa["roofline"]["scan_ms"]
+            alt["adc"]["roofline_frac"] = aa["roofline"]["frac"]
         log(f"[rank 0] alt data: {alt}")
         del Xa, ca
 

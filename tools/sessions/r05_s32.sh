@@ -1,0 +1,10 @@
+#!/bin/bash
+# round-5 session 32: ADC re-rank with the query LUT staged in LDS vs read from global memory:
+# ADC tests, interleaved A/B (M = 16 / 32, config #5 shape), outputs compared
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../..}"
+L=vector-quantization_amd/lib/ab
+bash tools/gpu_session.sh \
+  "python -u -m pytest tests/test_adc_filtered_gpu.py tests/test_kernels_gpu.py -m gpu -q -x -rf -k 'adc or filtered' --timeout 300 --timeout-method thread" \
+  "python -u tools/ab_lib.py $L/libmivq_rr0.so --what adc --reps 8" \
+  "python -u tools/ab_lib.py $L/libmivq_rr0.so --what adc --M 32 --reps 8" \
+  "python -u tools/ab_lib.py $L/libmivq_rr0.so --what adc --n 6650000 --d 1024 --reps 4"

@@ -143,3 +143,24 @@ def test_bench_two_ranks_one_gpu(dev, tmp_path):
     assert out["adc"]["n_total"] == 200000 and out["adc"]["topk_agreement_adc_vs_decode_exact"] >= 0.99
     c5 = out["config5"]
     assert c5["n_gpus"] == 2 and c5["rows_total"] == 120000 and c5["adc"]["topk_agreement_adc_vs_decode_exact"] >= 0.99
+
+
+@pytest.mark.gpu
+def test_rccl_collectives_world1(dev, tmp_path):
+    """RCCL on the hardware: an "nccl" process group of world size 1 on the card runs every
+    collective the multi-GPU path issues (broadcast, broadcast_object_list, all_gather_into_tensor
+    + mivq_topk_merge, all_reduce MAX) on device tensors; each must return its input.  Two ranks
+    cannot share one GPU under RCCL, so the multi-rank tests above use gloo."""
+    from haag_vq.parallel.launch import free_port
+
+    res_file = tmp_path / "rccl.json"
+    env = dict(os.environ, PYTHONPATH=str(PKG), HSA_ENABLE_IPC_MODE_LEGACY="0", MASTER_ADDR="127.0.0.1",
+               MASTER_PORT=str(free_port()), RANK="0", LOCAL_RANK="0", WORLD_SIZE="1")
+    env.pop("VQ_DIST_BACKEND", None)
+    p = subprocess.run([sys.executable, "-u", str(ROOT / "tests" / "_rccl_worker.py"), str(res_file)],
+                       capture_output=True, text=True, env=env, timeout=180, cwd=str(tmp_path))
+    assert p.returncode == 0, p.stdout[-3000:] + p.stderr[-3000:]
+    res = json.loads(res_file.read_text())
+    assert res["backend"] == "nccl" and res["world"] == 1
+    assert res["broadcast_equal"] and res["object_equal"] and res["allgather_merge_equal"]
+    assert res["sizes"] == [123457] and res["allreduce_max"] == 1.25

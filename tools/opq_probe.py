@@ -20,7 +20,7 @@ def main():
     ap.add_argument("--d", type=int, default=1536)
     ap.add_argument("--reps", type=int, default=5)
     ap.add_argument("--lib-gemm", action="store_true",
-                    help="also time one plain f16 / bf16 library GEMM (torch.matmul) of the same shape")
+                    help="also time plain f16 / bf16 / fp32 library GEMMs (torch.matmul) of the same shape")
     a = ap.parse_args()
     dev = _native.require_device()
     g = torch.Generator(device=dev).manual_seed(0)
@@ -40,8 +40,8 @@ def main():
     torch.cuda.synchronize()
     ms = s.elapsed_time(e) / a.reps
     print(f"opq rotate {a.n}x{a.d}: {ms:.3f} ms/call = {2 * a.n * a.d * a.d / (ms * 1e-3) / 1e12:.1f} TF/s", flush=True)
-    if a.lib_gemm:  # a yardstick: what one library f16 GEMM of this shape costs
-        for dt in (torch.float16, torch.bfloat16):
+    if a.lib_gemm:  # yardsticks: one library GEMM of this shape in f16 / bf16 / fp32
+        for dt in (torch.float16, torch.bfloat16, torch.float32):
             xh, bh = x.to(dt), A.to(dt)
             for _ in range(2):
                 torch.matmul(xh, bh)

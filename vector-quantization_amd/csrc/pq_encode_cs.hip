@@ -60,9 +60,12 @@ constexpr int kGcListNc = 4;  // wide-subspace resolve: pieces of a centroid row
 constexpr int kWideWaves = 4;
 constexpr int cs_waves(int KS) { return KS <= 6 ? kWaves : kWideWaves; }
 constexpr int kRsrcWord3 = 0x00020000;  // gfx9 buffer resource: 32-bit data format
-// x stream cache policy: nt (read once).  Rounds 4-5 measured the others, also for the dsub-48
-// filter alone (whose odd subspaces share a cache line with their neighbour): no gain.
+// x stream cache policy: nt (read once).  Rounds 4-5 measured the others.  The
+// dsub-48 filter, whose odd subspaces share a 128-B line with their neighbour, reads with sc0
+// instead: 8.12 -> 7.54 GB per PQ32 1M x 1536 launch (PMC FETCH_SIZE) and 1.753 -> 1.738 ms per
+// call back to back, codes identical (profiles/r05_s35; policy 0: 7.56 GB, 1.742 ms).
 constexpr int kXAux = 2;
+constexpr int kXAux48 = 1;
 // Byte of (row, subspace m) in the (M, n) code scratch (transposed once at the end).  Round 5
 // measured the codes stored in the (n, M) output directly (1-B stores 16 B apart, no transpose
 // launch): no faster per call.
@@ -312,7 +315,8 @@ __global__ __launch_bounds__(NW * 64) void pq_encode_cs_kernel(
                 // the block's uniform offset goes in soffset (SALU; gfx950 range-checks
                 // voffset + soffset, tools/probes/soffset_range.hip), the lane's in voffset
                 const int so = (vb * 32 + ibase(i)) * XS * 4 + hh * (16 * KT * 4);
-                const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(xr_rsrc, voff[i % PER], so, kXAux);
+                const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(xr_rsrc, voff[i % PER], so,
+                                                                      DS == 48 ? kXAux48 : kXAux);
                 dst[i] = make_float4(__uint_as_float(v[0]), __uint_as_float(v[1]), __uint_as_float(v[2]),
                                      __uint_as_float(v[3]));
             }

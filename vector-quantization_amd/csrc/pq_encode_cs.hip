@@ -63,7 +63,8 @@ constexpr int kRsrcWord3 = 0x00020000;  // gfx9 buffer resource: 32-bit data for
 // x stream cache policy: nt (read once).  Rounds 4-5 measured the others.  The
 // dsub-48 filter, whose odd subspaces share a 128-B line with their neighbour, reads with sc0
 // instead: 8.12 -> 7.54 GB per PQ32 1M x 1536 launch (PMC FETCH_SIZE) and 1.753 -> 1.738 ms per
-// call back to back, codes identical (profiles/r05_s35; policy 0: 7.56 GB, 1.742 ms).
+// call back to back, codes identical (profiles/r05_s35; policy 0: 7.56 GB, 1.742 ms).  For the
+// other shapes sc0 is slower (r05_s36: dsub 96 1.35 -> 1.45 ms, dsub 64 -3 %, dsub 192 -11 %).
 constexpr int kXAux = 2;
 constexpr int kXAux48 = 1;
 // Byte of (row, subspace m) in the (M, n) code scratch (transposed once at the end).  Round 5

@@ -1,0 +1,9 @@
+#!/bin/bash
+# round-5 session 37 (final sources: LDS re-rank, dsub-48 sc0): full GPU suite, smoke, PMC traffic passes
+# (profiles/traffic.json), kernel-trace splits by call size at 1M and 10M rows, the default bench
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../..}"
+bash tools/gpu_session.sh pytest smoke \
+  "bash tools/pmc_traffic.sh" \
+  "bash tools/prof_split.sh r05_1m --steps 5 --warmup 2" \
+  "bash tools/prof_split.sh r05_10m --n 10000000 --no-adc --steps 3 --warmup 1" \
+  "python -u bench.py"

@@ -1,5 +1,5 @@
 #!/bin/bash
-# round-5 session 33 (final sources, LDS re-rank): full GPU suite, smoke, PMC traffic passes
+# round-5 session 37 (final sources: LDS re-rank, dsub-48 sc0): full GPU suite, smoke, PMC traffic passes
 # (profiles/traffic.json), kernel-trace splits by call size at 1M and 10M rows, the default bench
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../..}"
 bash tools/gpu_session.sh pytest smoke \

@@ -1,7 +1,7 @@
 #!/bin/bash
-# round-5 session 30 (final sources): full GPU suite, smoke, PMC traffic passes
+# Round-end evidence session (round 5: session 37, profiles/r05_final): full GPU suite, smoke, PMC traffic passes
 # (profiles/traffic.json), kernel-trace splits by call size at 1M and 10M rows, the default bench
-cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../..}"
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 bash tools/gpu_session.sh pytest smoke \
   "bash tools/pmc_traffic.sh" \
   "bash tools/prof_split.sh r05_1m --steps 5 --warmup 2" \

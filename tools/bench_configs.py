@@ -105,6 +105,7 @@ def main():
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--opq-iters", type=int, default=10)
     ap.add_argument("--data", choices=("gaussian", "clustered"), default="clustered")
+    ap.add_argument("--cpu-seconds", type=float, default=10.0, help="target CPU-baseline work (bench.py's option)")
     a = ap.parse_args()
     dev = _native.require_device()
     if a.workload == "opq32":

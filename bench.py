@@ -715,6 +715,37 @@ def dry_run(a):
 
 
 # ------------------------------------------------------------------------- main
+def summary_of(out, k):
+    """Compact digest of the bench line: the encode headline and the ADC headline (queries/s,
+    recall@k, roofline frac), and the same few figures of the north-star, config #5 and
+    configs legs."""
+    def r(x, n=4):
+        return None if x is None else round(float(x), n)
+
+    def adc_digest(ad):
+        if not ad:
+            return None
+        rf = ad.get("roofline") or {}
+        return {"qps": r(ad["qps"], 0), f"recall@{k}": r(ad.get(f"recall@{k}")), "frac": r(rf.get("frac")),
+                "bound": rf.get("bound"), "scan_ms": r(rf.get("scan_ms"))}
+
+    sm = {"encode_vps": r(out["value"], 0), "encode_frac": r(out["roofline"]["frac"]),
+          "parity_mismatched_codes": (out.get("parity_sample") or {}).get("mismatched_codes"),
+          "adc": adc_digest(out.get("adc"))}
+    ns = out.get("north_star")
+    if ns:
+        sm["north_star"] = {"vps": r(ns["value"], 0), "frac": r(ns["roofline"]["frac"])}
+    c5 = out.get("config5")
+    if c5:
+        sm["config5"] = {"vps_per_gpu": r(c5.get("value_per_gpu", c5.get("value")), 0),
+                         "frac": r((c5.get("roofline") or {}).get("frac")), "adc": adc_digest(c5.get("adc"))}
+    cf = out.get("configs") or {}
+    for name, leg in cf.items():
+        if isinstance(leg, dict):
+            sm[name] = {"value": r(leg.get("value"), 0), "frac": r((leg.get("roofline") or {}).get("frac"))}
+    return sm
+
+
 def main():
     a = parse()
     env_world = os.environ.get("WORLD_SIZE")
@@ -859,6 +890,9 @@ def main():
             "config5": c5,
             "configs": configs,
         }
+        # LAST key (a driver keeps the tail of this one long line): the headline numbers of
+        # every leg in a few hundred bytes
+        out["summary"] = summary_of(out, a.k)
         print(json.dumps(out), flush=True)
     if world > 1:
         dist.destroy_process_group()

@@ -39,7 +39,7 @@ extern "C" {
 #define MIVQ_ERR_HIP (-3)         /* HIP runtime / launch failure    -> RuntimeError */
 #define MIVQ_ERR_WORKSPACE (-4)   /* workspace too small             -> RuntimeError */
 
-#define MIVQ_ABI_VERSION 1
+#define MIVQ_ABI_VERSION 2 /* 2: mivq_adc_search takes flags */
 
 /* PQ encode flags */
 #define MIVQ_PQ_AUTO 0u        /* fp16-MFMA candidate filter + exact fp32 re-check when supported */
@@ -199,10 +199,18 @@ int mivq_extrabitq_rotate(const double* o, int64_t n, int32_t d, const double* P
 int mivq_adc_lut(const float* q, int64_t nq, int32_t d, int32_t M, int32_t nbits,
                  const float* centroids, int32_t metric, float* lut, void* stream);
 size_t mivq_adc_search_workspace_bytes(int64_t nq, int64_t n, int32_t M, int32_t nbits, int32_t k);
-/* codes: (n, M) one byte per sub-code (nbits <= 8; use mivq_pq_unpack for nbits < 8). */
+/* codes: (n, M) one byte per sub-code (nbits <= 8; use mivq_pq_unpack for nbits < 8).
+ * flags: MIVQ_ADC_AUTO (0) for every product call; the other bits are diagnostics / test
+ * hooks and change no result except MIVQ_ADC_NO_RERUN (see below).  The workspace size does
+ * not depend on flags. */
+#define MIVQ_ADC_AUTO 0u          /* filtered search where the shape allows it, else the fp32 scan */
+#define MIVQ_ADC_FORCE_EXACT 1u   /* diagnostic: the fp32 scan for every query (same results)      */
+#define MIVQ_ADC_NO_RERUN 2u      /* test hook: queries the filter cannot certify are left NaN      */
+#define MIVQ_ADC_SMALL_RERUN_GRID 4u /* test hook: the re-run of uncertified queries on one column of
+                                        workgroups, each walking several list-slot blocks          */
 int mivq_adc_search(const float* lut, int64_t nq, const uint8_t* codes, int64_t n, int32_t M,
                     int32_t nbits, int32_t k, int64_t id_offset, void* workspace,
-                    size_t workspace_bytes, float* dists, uint32_t* ids, void* stream);
+                    size_t workspace_bytes, float* dists, uint32_t* ids, uint32_t flags, void* stream);
 /* Exact brute-force top-k over an f32 database (the decode-then-search path of
  * FlatQuantizedIndex for SQ / RaBitQ reconstructions, flat_quantized_index.py:57-76):
  *   L2: dist = fmaf chain over t of (q_t - x_t)^2;  IP: dist = -(fmaf chain of q_t * x_t)

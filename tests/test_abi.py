@@ -29,7 +29,7 @@ def test_library_exports_every_declared_symbol():
     for name in _declared():
         assert hasattr(lib, name), name
     assert set(_declared()) == set(_native.SIGNATURES), "ctypes table out of sync with mivq.h"
-    assert lib.mivq_abi_version() == 1
+    assert lib.mivq_abi_version() == 2
 
 
 def test_size_queries_need_no_gpu():
@@ -90,3 +90,16 @@ def test_no_packed_fp32_on_lds_loads():
               "adc_rerank_kernel", "opq_split_gemm_kernel", "pairwise_kernel"):
         assert any(k in w for w in walked), (k, len(walked))  # the audit really read the library
     assert not findings, {k[:80]: v[:2] for k, v in findings.items()}
+
+
+def test_adc_search_workspace_bounded():
+    """The filtered search's part lists and the re-run's lists are bounded: 10M rows
+    x 10,000 queries at k = 32 needs well under a gigabyte (unbounded re-run lists: ~10.5 GB),
+    100,000 queries stay within a few GB (the output alone is 25.6 MB per 1,000 queries)."""
+    from haag_vq import _native
+
+    lib = _native.load_library()
+    nb = lib.mivq_adc_search_workspace_bytes(10_000, 10_000_000, 16, 8, 32)
+    assert 0 < nb < 800 * 2 ** 20, nb
+    nb = lib.mivq_adc_search_workspace_bytes(100_000, 10_000_000, 16, 8, 32)
+    assert 0 < nb < 3 * 2 ** 30, nb

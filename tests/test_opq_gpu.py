@@ -199,6 +199,25 @@ def test_polar_factor_newton_schulz(dev):
 
 
 @pytest.mark.gpu
+def test_polar_factor_small_singular_tail_stays_on_newton_schulz(dev):
+    """ones plus 8 singular values at 1e-3 (a tail of low-variance directions) hold
+    ||Q^T Q - I|| near sqrt(8) for ~17 steps while they grow 1.5x per step.  That is not rank
+    deficiency: the iteration must go on to the polar factor, not to the SVD."""
+    from haag_vq.methods.optimized_product_quantization import polar_factor
+
+    rng = np.random.default_rng(12)
+    d = 128
+    U, _ = np.linalg.qr(rng.standard_normal((d, d)))
+    V, _ = np.linalg.qr(rng.standard_normal((d, d)))
+    S = np.ones(d)
+    S[-8:] = 1e-3
+    G = (U * S) @ V.T
+    info = {}
+    Q = polar_factor(_t(G, dev), info=info).cpu().numpy()
+    assert info["path"] == "newton-schulz", info
+    np.testing.assert_allclose(Q, U @ V.T, atol=1e-9)
+
+
 def test_polar_factor_top_vector_orthogonal_to_ones(dev):
     """G whose dominant right singular vector is orthogonal to the all-ones vector
     and whose top two singular values are 2 : 1.  A start scale estimated from below (a power

@@ -124,3 +124,82 @@ def test_streaming_sweep_local_file(tmp_path):
     pq.fit(X[:5000])
     rec = pq.decompress(pq.compress(X))
     assert m["mse"] == pytest.approx(float(((X.astype(np.float64) - rec) ** 2).sum(1).mean()), rel=1e-6)
+
+
+def test_streaming_sweep_grouped_calls_equal_per_batch_calls(tmp_path, monkeypatch):
+    """The device encode takes several stream batches per call (streaming_sweep.CALL_ROWS); the
+    logged row must equal the one of upstream's one-call-per-batch loop bit for bit (ragged
+    last batch and a group boundary inside the run included)."""
+    from typer.testing import CliRunner
+
+    from haag_vq.benchmarks import streaming_sweep as ss
+    from haag_vq.cli import app
+
+    X = np.random.default_rng(6).standard_normal((23_456, 96)).astype(np.float32)
+    np.save(tmp_path / "stream.npy", X)
+    out = {}
+    for tag, rows in (("per_batch", 3000), ("grouped", 9000), ("one_call", 1 << 20)):
+        monkeypatch.setattr(ss, "CALL_ROWS", rows)
+        db = tmp_path / f"{tag}.db"
+        res = CliRunner().invoke(app, ["streaming-sweep", "--method", "pq", "--pq-subquantizers", "8",
+                                       "--training-size", "4096", "--batch-size", "3000",
+                                       "--data-path", str(tmp_path / "stream.npy"), "--db-path", str(db)])
+        assert res.exit_code == 0, res.output + repr(res.exception)
+        con = sqlite3.connect(db)
+        (mj,), = con.execute("SELECT metrics_json FROM runs").fetchall()
+        con.close()
+        out[tag] = json.loads(mj)
+    assert ss.batches_per_call(3000, 96) == (1 << 20) // 3000
+    for tag in ("grouped", "one_call"):
+        assert out[tag]["mse"] == out["per_batch"]["mse"]
+        assert out[tag]["num_batches"] == out["per_batch"]["num_batches"] == 8
+        assert out[tag]["total_vectors_compressed"] == 23_456
+
+
+def test_sweep_config1_standin_shape(tmp_path, monkeypatch, oracle):
+    """BASELINE config #1's shape through the caller (SURVEY §8d row 1's stand-in for the
+    offline dbpedia-100k): `sweep --dataset dbpedia-100k --method pq --pq-subquantizers 8
+    --pq-bits 8` on a local 100k x 1536 unit-normalised Gaussian file (seed 0).  The logged row
+    has the reference's schema and metric set, compression ratio 4 D / M = 768 (row 56), and the
+    PQ8 (dsub 192) codes of a 20k-row sample equal the oracle's canonical encode under the
+    codebook the sweep trained."""
+    from typer.testing import CliRunner
+
+    import torch
+    from haag_vq.benchmarks import sweep as sw
+    from haag_vq.cli import app
+
+    X = np.random.default_rng(0).standard_normal((100_000, 1536), dtype=np.float32)
+    X /= np.linalg.norm(X, axis=1, keepdims=True)
+    np.save(tmp_path / "dbpedia-100k.npy", X)
+    models = []
+    build = sw._build_model
+
+    def capture(method, config):
+        models.append(build(method, config))
+        return models[-1]
+
+    monkeypatch.setattr(sw, "_build_model", capture)
+    db = tmp_path / "runs.db"
+    res = CliRunner().invoke(app, ["sweep", "--dataset", "dbpedia-100k", "--cache-dir", str(tmp_path), "--method",
+                                   "pq", "--pq-subquantizers", "8", "--pq-bits", "8", "--db-path", str(db),
+                                   "--codebooks-dir", str(tmp_path / "cb")])
+    assert res.exit_code == 0, res.output + repr(res.exception)
+    con = sqlite3.connect(db)
+    cols = [r[1] for r in con.execute("PRAGMA table_info(runs)")]
+    (method, dataset, mj, cj), = con.execute("SELECT method, dataset, metrics_json, config_json FROM runs").fetchall()
+    con.close()
+    assert cols == REF_COLUMNS and (method, dataset) == ("pq", "dbpedia-100k")
+    m = json.loads(mj)
+    assert json.loads(cj) == {"name": "PQ(subquantizers=8, bits=8)", "subquantizers": 8, "bits": 8}
+    assert m["compression_ratio"] == 768.0
+    for key in ("reconstruction_distortion", "recall@10", "recall@100", "qps", "rank_distortion@10",
+                "pairwise_distortion_mean", "roofline_frac", "encode_device_ms"):
+        assert key in m, key
+    assert 0.0 < m["recall@10"] <= 1.0 and m["n_gpus"] == 1
+    pq, = models
+    C = pq.centroids_device.cpu().numpy()
+    assert C.shape == (8, 256, 192)
+    got = pq.compress(torch.from_numpy(X[:20_000]).cuda())
+    got = got.cpu().numpy() if hasattr(got, "cpu") else np.asarray(got)
+    np.testing.assert_array_equal(got, oracle.pq_encode(X[:20_000], C))

@@ -100,7 +100,7 @@ def main():
         def run_adc(k):
             ws, od, oi = adc[k]
             rc = libs[k].mivq_adc_search(P(lut.data_ptr()), a.nq, P(codes.data_ptr()), a.n, a.M, 8, a.k, 0,
-                                         P(ws.data_ptr()), ws.numel(), P(od.data_ptr()), P(oi.data_ptr()), P(st))
+                                         P(ws.data_ptr()), ws.numel(), P(od.data_ptr()), P(oi.data_ptr()), 0, P(st))
             assert rc == 0, rc
 
         run = run_adc

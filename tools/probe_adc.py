@@ -1,11 +1,10 @@
-"""Interleaved timing of mivq_adc_search: the filtered path vs the fp32 scan (MIVQ_ADC_EXACT=1),
+"""Interleaved timing of mivq_adc_search: the filtered path vs the fp32 scan (flag MIVQ_ADC_FORCE_EXACT),
 same process and data; checks ids / distances identical.
 
 usage: python tools/probe_adc.py [--n 1000000] [--nq 1000] [--M 16] [--k 10] [--reps 10] [--data gaussian]
 Codes are the PQ encode of synthetic rows (bench.synth) with k-means codebooks, as in bench.py.
 """
 import argparse
-import os
 import sys
 from pathlib import Path
 
@@ -39,11 +38,7 @@ def main():
     lut = _native.adc_lut(Q, C, 8, _native.METRIC_L2)
 
     def run(exact):
-        if exact:
-            os.environ["MIVQ_ADC_EXACT"] = "1"
-        else:
-            os.environ.pop("MIVQ_ADC_EXACT", None)
-        return _native.adc_search(lut, codes, a.k, 8)
+        return _native.adc_search(lut, codes, a.k, 8, flags=_native.ADC_FORCE_EXACT if exact else _native.ADC_AUTO)
 
     fd, fi = run(False)
     ed, ei = run(True)

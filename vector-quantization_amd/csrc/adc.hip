@@ -581,10 +581,13 @@ __global__ __launch_bounds__(256) void adc_qstats_kernel(const float* __restrict
     }
 }
 
-// grid (ceil(nq / QB), M), block 256 (code c): table block b = (M, 256, QB / 4) dwords; dword
-// w holds queries (4w, 4w + 2, 4w + 1, 4w + 3) in bytes 0..3, so the two byte-pair unpacks
-// give the u16 pairs (4w, 4w + 1) and (4w + 2, 4w + 3).  q <= (lut - min) / delta (the ratio
-// is shrunk by 2^-50 before the floor, so fp64 rounding never rounds it up past an integer).
+// grid (ceil(nq / QB), M), block 256 (code c): one 16-B entry per (m, c) holding the 16 queries'
+// bytes; dword w holds queries (4w, 4w + 2, 4w + 1, 4w + 3) in bytes 0..3, so the two byte-pair
+// unpacks give the u16 pairs (4w, 4w + 1) and (4w + 2, 4w + 3).  q <= (lut - min) / delta (the
+// ratio is shrunk by 2^-50 before the floor, so fp64 rounding never rounds it up past an
+// integer).  Entry order (round 6): [m / 16][c][m % 16] -- the 16 subspaces of a half side by
+// side in one 256-B bank row per code, so that lanes reading 16 DIFFERENT subspaces hit 16
+// different bank slots whatever their codes (adc_qscan_kernel).
 template <int QB>
 __global__ __launch_bounds__(256) void adc_qtab_kernel(const float* __restrict__ lut, int64_t nq, int M,
                                                        const float* __restrict__ mins,
@@ -611,7 +614,7 @@ __global__ __launch_bounds__(256) void adc_qtab_kernel(const float* __restrict__
         const int r = qq & 3;
         w[qq >> 2] |= v << (8 * (((r & 1) << 1) | (r >> 1)));
     }
-    uint32_t* dst = tab + ((qb * M + m) * 256 + c) * NWD;
+    uint32_t* dst = tab + (((qb * (M / 16) + (m >> 4)) * 256 + c) * 16 + (m & 15)) * NWD;
     if constexpr (NWD >= 4) {
 #pragma unroll
         for (int j = 0; j < NWD; j += 4) *reinterpret_cast<uint4*>(dst + j) = make_uint4(w[j], w[j + 1], w[j + 2], w[j + 3]);
@@ -674,6 +677,34 @@ __global__ __launch_bounds__(kScanWaves * 64) void adc_qscan_kernel(
 #pragma unroll
         for (int c = 0; c < MC; ++c) cw[c] = row < rend ? cr[c] : make_uint4(0u, 0u, 0u, 0u);
     };
+    // Conflict-free lookups (round 6).  A ds_read_b128 is served in four 16-lane groups, one LDS
+    // cycle per group when its 16 lanes hit 16 different 16-B slots of the 256-B bank row
+    // (MI355X_MICROARCH.md §LDS); with the table [m][code], slot = code % 16 is random and a group
+    // took ~3 cycles.  With the table [m / 16][code][m % 16] the slot is m % 16, so at every
+    // lookup step the lanes of a group read 16 different subspaces: lane l (r = l % 16, rd = r / 4,
+    // rb = r % 4; every 16-lane group of ds_read_b128 holds each r once) takes at step (word k,
+    // byte b) subspace mm = 4 ((k + rd) % 4) + (b + rb) % 4 of the half.  The integer sums do
+    // not depend on the order of their terms.  Per lookup the address is still ONE VALU: a
+    // v_perm builds code << 8 | mm << 4 from the code word (byte (b + rb) % 4 of its dword
+    // rotated by rd) and a per-lane register of the four mm << 4 values of word k.
+    const uint32_t rl = (uint32_t)lane & 15u, rd = rl >> 2, rb = rl & 3u;
+    uint32_t mo[4], psel[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        uint32_t v = 0u;
+#pragma unroll
+        for (int b = 0; b < 4; ++b) v |= ((4u * ((k + rd) & 3u) + ((b + rb) & 3u)) << 4) << (8 * b);
+        mo[k] = v;
+    }
+#pragma unroll
+    for (int b = 0; b < 4; ++b)  // byte0 <- mo byte b (S1), byte1 <- code byte (b + rb) % 4 (S0), bytes 2, 3 <- 0
+        psel[b] = (uint32_t)b | ((4u + ((b + rb) & 3u)) << 8) | 0x0C0C0000u;
+    // the code row's dwords rotated by rd within each 16-B half (two select levels)
+    auto rot = [&](uint4 w) __attribute__((always_inline)) {
+        const bool r1 = (rd & 1u) != 0u, r2 = (rd & 2u) != 0u;
+        const uint32_t t0 = r1 ? w.y : w.x, t1 = r1 ? w.z : w.y, t2 = r1 ? w.w : w.z, t3 = r1 ? w.x : w.w;
+        return make_uint4(r2 ? t2 : t0, r2 ? t3 : t1, r2 ? t0 : t2, r2 ? t1 : t3);
+    };
     // entries of kAdcBits < 8 bits: 2^(8 - bits) lookups add up in the bytes themselves (no carry
     // crosses a byte) before one unpack to the u16 pairs
     constexpr int UNP = 1 << (8 - kAdcBits);
@@ -693,32 +724,24 @@ __global__ __launch_bounds__(kScanWaves * 64) void adc_qscan_kernel(
         uint32_t wq[4 * MC];
 #pragma unroll
         for (int c = 0; c < MC; ++c) {
+            cur[c] = rot(cur[c]);
             wq[4 * c + 0] = cur[c].x; wq[4 * c + 1] = cur[c].y;
             wq[4 * c + 2] = cur[c].z; wq[4 * c + 3] = cur[c].w;
         }
         // unrolled over the code words (round 5: 0.560 -> 0.531 ms per 1000 x 1M at M = 16,
-        // profiles/r05_s20): word jw is wq[jw] and its subspaces' table offset rides in the
-        // ds_read immediate, instead of a register shift of wq and an address add per word
+        // profiles/r05_s20): word jw is read straight from its register wq[jw]
         uint32_t a8[4] = {0u, 0u, 0u, 0u};  // byte sums of up to UNP lookups (across words)
 #pragma unroll
         for (int jw = 0; jw < 4 * MC; ++jw) {
             const uint32_t wrd = wq[jw];
-            const int jofs = jw * 4 * 256;  // in 16-B entries
 #pragma unroll
             for (int b = 0; b < 4; ++b) {
-                // code byte b << 4 in ONE op (SDWA byte select on the shifted operand), used as
-                // the LDS address itself: qt is this kernel's only LDS, so the dynamic segment
-                // starts at address 0 (guarded at the bound store below)
-                uint32_t o1;
-                if (b == 0)
-                    asm("v_lshlrev_b32_sdwa %0, 4, %1 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:BYTE_0" : "=v"(o1) : "v"(wrd));
-                else if (b == 1)
-                    asm("v_lshlrev_b32_sdwa %0, 4, %1 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:BYTE_1" : "=v"(o1) : "v"(wrd));
-                else if (b == 2)
-                    asm("v_lshlrev_b32_sdwa %0, 4, %1 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:BYTE_2" : "=v"(o1) : "v"(wrd));
-                else
-                    asm("v_lshlrev_b32_sdwa %0, 4, %1 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:BYTE_3" : "=v"(o1) : "v"(wrd));
-                const u32x4v t0 = *(reinterpret_cast<const lds_u4*>((uintptr_t)o1) + jofs + b * 256);
+                // code << 8 | mm << 4 in ONE v_perm; the half's 64 KiB (M = 32) is one more op
+                // (the ds_read offset field holds 16 bits); qt is this kernel's only LDS, so the
+                // dynamic segment starts at address 0 (guarded at the bound store below)
+                uint32_t o1 = __builtin_amdgcn_perm(wrd, mo[jw & 3], psel[b]);
+                if (jw >= 4) o1 |= (uint32_t)(jw >> 2) << 16;
+                const u32x4v t0 = *(reinterpret_cast<const lds_u4*>((uintptr_t)o1));
                 const uint32_t tv[4] = {t0.x, t0.y, t0.z, t0.w};
 #pragma unroll
                 for (int wd = 0; wd < 4; ++wd) a8[wd] = ((4 * jw + b) % UNP == 0) ? tv[wd] : a8[wd] + tv[wd];
@@ -901,7 +924,8 @@ int adc_qb(int M, int ksub) {
 // per CU, so the grid of nch * qblocks workgroups takes ceil(nch * qblocks / 256) rounds, each
 // as long as one workgroup's table fill (about half a wave-step of 1024 rows) plus its
 // ceil(n / nch / 1024) wave-steps: pick the nch of least total time (the smallest on ties:
-// fewer partial lists).  nq = 1000 at QB = 8, n = 1M: 2 chunks, 250 workgroups in one round,
+// fewer partial lists; a larger count must gain 2 %: the model is coarse, and every chunk adds
+// a part list per query).  nq = 1000 at QB = 8, n = 1M: 2 chunks, 250 workgroups in one round,
 // instead of 625 in three of which the last is 44 % full.
 int64_t adc_chunks(int64_t nq, int64_t n, int QB) {
     const int64_t qblocks = ceil_div(nq, QB);
@@ -911,7 +935,7 @@ int64_t adc_chunks(int64_t nq, int64_t n, int QB) {
     double best_cost = 0.0;
     for (int64_t nch = 1; nch <= cap; ++nch) {
         const double cost = (double)ceil_div(nch * qblocks, 256) * ((double)ceil_div(ceil_div(n, nch), step_rows) + 0.5);
-        if (nch == 1 || cost < best_cost * (1.0 - 1e-9)) { best = nch; best_cost = cost; }
+        if (nch == 1 || cost < best_cost * 0.98) { best = nch; best_cost = cost; }
     }
     return best;
 }
@@ -919,7 +943,7 @@ int64_t adc_chunks(int64_t nq, int64_t n, int QB) {
 template <int R, int QB>
 hipError_t launch_scan(const float* lut, int64_t nq, const uint8_t* codes, int64_t n, int M, int ksub, int k,
                        int64_t id_offset, int64_t nch, float* pd, uint32_t* pi, hipStream_t st,
-                       const int* qlist = nullptr, const int* qcount = nullptr) {
+                       const int* qlist = nullptr, const int* qcount = nullptr, bool small_grid = false) {
     const size_t smem = (size_t)QB * M * ksub * sizeof(float);
     const bool vec = ksub == 256 && reinterpret_cast<uintptr_t>(codes) % 16 == 0;
     auto kern = vec && M == 16 ? adc_scan_kernel<R, QB, 1> : vec && M == 32 ? adc_scan_kernel<R, QB, 2>
@@ -928,7 +952,8 @@ hipError_t launch_scan(const float* lut, int64_t nq, const uint8_t* codes, int64
     if (e != hipSuccess) return e;
     const int64_t chunk_rows = ceil_div(n, nch);
     // the re-run of uncertified queries: one round of workgroups looping over the list slots
-    const int64_t qgrid = qlist != nullptr ? std::max<int64_t>(1, std::min<int64_t>(ceil_div(nq, QB), 256 / nch))
+    // (small_grid, a test hook: one column, so every workgroup walks several slot blocks)
+    const int64_t qgrid = qlist != nullptr ? (small_grid ? 1 : std::max<int64_t>(1, std::min<int64_t>(ceil_div(nq, QB), 256 / nch)))
                                            : ceil_div(nq, QB);
     hipLaunchKernelGGL(kern, dim3((unsigned)nch, (unsigned)qgrid), dim3(kScanWaves * 64), smem, st, lut, nq, codes,
                        n, M, ksub, k, id_offset, chunk_rows, pd, pi, qlist, qcount);
@@ -936,18 +961,28 @@ hipError_t launch_scan(const float* lut, int64_t nq, const uint8_t* codes, int64
 }
 
 // Row chunks of the re-run of uncertified queries: ~32k rows each (one failed query costs a
-// few tens of microseconds, not a whole-database workgroup).
-int64_t adc_fallback_chunks(int64_t n) { return std::max<int64_t>(1, std::min<int64_t>(256, ceil_div(n, 32768))); }
+// few tens of microseconds, not a whole-database workgroup), as long as the re-run's part
+// lists -- sized for every query, since the host does not know how many fail -- stay within
+// kRerunListBytes: (16 parts per chunk) x nq x k x 8 B per chunk.  At nq = 10,000, k = 32 that
+// is 40 MB per chunk, so 6 chunks (a failed query then scans ~1/6 of the rows per workgroup:
+// slower, never wrong); below 1,000 queries at k = 10 the 256 chunks fit.  (the
+// unbounded form sized 10.5 GB at n = 10M, nq = 10k, k = 32.)
+constexpr size_t kRerunListBytes = size_t(256) << 20;
+int64_t adc_fallback_chunks(int64_t nq, int64_t n, int k) {
+    const int64_t want = std::max<int64_t>(1, std::min<int64_t>(256, ceil_div(n, 32768)));
+    const size_t per_chunk = (size_t)kScanWaves * (size_t)std::max<int64_t>(nq, 1) * (size_t)k * 8u;
+    return std::max<int64_t>(1, std::min<int64_t>(want, (int64_t)(kRerunListBytes / per_chunk)));
+}
 
 template <int R>
 hipError_t launch_scan_r(int QB, const float* lut, int64_t nq, const uint8_t* codes, int64_t n, int M, int ksub,
                          int k, int64_t id_offset, int64_t nch, float* pd, uint32_t* pi, hipStream_t st,
-                         const int* qlist = nullptr, const int* qcount = nullptr) {
+                         const int* qlist = nullptr, const int* qcount = nullptr, bool sg = false) {
     switch (QB) {
-        case 8: return launch_scan<R, 8>(lut, nq, codes, n, M, ksub, k, id_offset, nch, pd, pi, st, qlist, qcount);
-        case 4: return launch_scan<R, 4>(lut, nq, codes, n, M, ksub, k, id_offset, nch, pd, pi, st, qlist, qcount);
-        case 2: return launch_scan<R, 2>(lut, nq, codes, n, M, ksub, k, id_offset, nch, pd, pi, st, qlist, qcount);
-        default: return launch_scan<R, 1>(lut, nq, codes, n, M, ksub, k, id_offset, nch, pd, pi, st, qlist, qcount);
+        case 8: return launch_scan<R, 8>(lut, nq, codes, n, M, ksub, k, id_offset, nch, pd, pi, st, qlist, qcount, sg);
+        case 4: return launch_scan<R, 4>(lut, nq, codes, n, M, ksub, k, id_offset, nch, pd, pi, st, qlist, qcount, sg);
+        case 2: return launch_scan<R, 2>(lut, nq, codes, n, M, ksub, k, id_offset, nch, pd, pi, st, qlist, qcount, sg);
+        default: return launch_scan<R, 1>(lut, nq, codes, n, M, ksub, k, id_offset, nch, pd, pi, st, qlist, qcount, sg);
     }
 }
 
@@ -983,8 +1018,8 @@ hipError_t launch_flat_r(int QB, const float* q, int64_t nq, const float* x, int
     }
 }
 
-// Filtered path eligibility by shape (the workspace is sized on shape alone) and the profiling
-// switch MIVQ_ADC_EXACT=1 (the fp32 scan for every query).
+// Filtered path eligibility by shape (the workspace is sized on shape alone; the diagnostic
+// flag MIVQ_ADC_FORCE_EXACT runs the fp32 scan for every query in the same workspace).
 // (queries per table block: the variants whose lists fit the 128 registers of the 16-wave scan)
 // Part lists keep K1 = k + kListSlack entries (at most 256): the certificate bounds the rows a
 // part did NOT list by its K1-th entry, so a part holding some of the k best rows still
@@ -992,7 +1027,7 @@ hipError_t launch_flat_r(int QB, const float* q, int64_t nq, const float* x, int
 // a k = 1 search never could).
 constexpr int kListSlack = 4;
 int adc_k1(int k) { return k + kListSlack; }
-// k <= 32: a part's 128 lane candidates (two per lane) carry the k best rows with room to spare;
+// k <= 32: a part's 192 lane candidates (kLaneKeys = 3 per lane) carry the k best rows with room to spare;
 // for larger k the per-lane bound (a lane's second-best) sits too close to the k-th distance to
 // certify, and the fp32 scan serves those searches
 bool adc_filtered_shape(int M, int ksub, int k) { return ksub == 256 && (M == 16 || M == 32) && k <= 32; }
@@ -1008,8 +1043,12 @@ AdcFilteredLayout adc_filtered_layout(int64_t nq, int64_t n, int M, int k, size_
     AdcFilteredLayout L{};
     const int QB = adc_fqb(M, k);
     L.k1 = adc_k1(k);
-    // a lane's step index is 16 bits: at most 65535 wave-steps (of 1024 rows) per chunk
-    L.nch = std::max<int64_t>(adc_chunks(nq, n, QB), ceil_div(n, (int64_t)65535 * kScanWaves * 64));
+    // the part lists stay within ~1 GiB where the chunk model would ask for more (100k queries:
+    // 2 chunks instead of 12, at the same modelled time), and a lane's step index is 16 bits: at
+    // most 65535 wave-steps (of 1024 rows) per chunk
+    const size_t per_chunk = (size_t)kScanWaves * (size_t)nq * (size_t)L.k1 * 8u;
+    const int64_t cap = std::max<int64_t>(1, (int64_t)((size_t(1) << 30) / per_chunk));
+    L.nch = std::max<int64_t>(std::min<int64_t>(adc_chunks(nq, n, QB), cap), ceil_div(n, (int64_t)65535 * kScanWaves * 64));
     L.parts = L.nch * kScanWaves;
     L.stats = off;  off = align_up(off + (size_t)nq * sizeof(AdcQStat), 256);
     L.mins = off;   off = align_up(off + (size_t)nq * M * sizeof(float), 256);
@@ -1176,7 +1215,7 @@ extern "C" size_t mivq_adc_search_workspace_bytes(int64_t nq, int64_t n, int32_t
     const int QB = adc_qb(M, 1 << nbits);
     if (QB == 0) return 0;
     int64_t parts = adc_chunks(nq, n, QB) * kScanWaves;
-    if (adc_filtered_shape(M, 1 << nbits, k)) parts = std::max<int64_t>(parts, adc_fallback_chunks(n) * kScanWaves);
+    if (adc_filtered_shape(M, 1 << nbits, k)) parts = std::max<int64_t>(parts, adc_fallback_chunks(nq, n, k) * kScanWaves);
     // the fp32 scan's part lists (every query, or the filtered path's uncertified ones) ...
     const size_t exact = align_up((size_t)parts * nq * k * sizeof(float), 256) + align_up((size_t)parts * nq * k * 4, 256);
     // ... then the filtered path's regions
@@ -1186,9 +1225,11 @@ extern "C" size_t mivq_adc_search_workspace_bytes(int64_t nq, int64_t n, int32_t
 
 extern "C" int mivq_adc_search(const float* lut, int64_t nq, const uint8_t* codes, int64_t n, int32_t M,
                                int32_t nbits, int32_t k, int64_t id_offset, void* workspace,
-                               size_t workspace_bytes, float* dists, uint32_t* ids, void* stream) {
+                               size_t workspace_bytes, float* dists, uint32_t* ids, uint32_t flags, void* stream) {
     MIVQ_REQUIRE(nq >= 0 && n >= 0 && M > 0 && k > 0, MIVQ_ERR_INVALID,
                  "adc_search: bad sizes nq=%lld n=%lld M=%d k=%d", (long long)nq, (long long)n, M, k);
+    MIVQ_REQUIRE((flags & ~(MIVQ_ADC_FORCE_EXACT | MIVQ_ADC_NO_RERUN | MIVQ_ADC_SMALL_RERUN_GRID)) == 0,
+                 MIVQ_ERR_INVALID, "adc_search: unknown flags 0x%x", flags);
     MIVQ_REQUIRE(nbits >= 1 && nbits <= 8, MIVQ_ERR_UNSUPPORTED, "adc_search: nbits=%d", nbits);
     MIVQ_REQUIRE(k <= 256, MIVQ_ERR_UNSUPPORTED, "adc_search: k=%d > 256", k);
     const int ksub = 1 << nbits;
@@ -1210,7 +1251,7 @@ extern "C" int mivq_adc_search(const float* lut, int64_t nq, const uint8_t* code
     MIVQ_REQUIRE(workspace && workspace_bytes >= need, MIVQ_ERR_WORKSPACE, "adc_search: workspace %zu < %zu",
                  workspace_bytes, need);
     const bool fshape = adc_filtered_shape(M, ksub, k);
-    const int64_t nch_exact = adc_chunks(nq, n, QB), nch_fb = adc_fallback_chunks(n);
+    const int64_t nch_exact = adc_chunks(nq, n, QB), nch_fb = adc_fallback_chunks(nq, n, k);
     const int64_t parts_ws = std::max<int64_t>(nch_exact, fshape ? nch_fb : 0) * kScanWaves;
     float* pd = static_cast<float*>(workspace);
     const size_t exact_bytes = align_up((size_t)parts_ws * nq * k * sizeof(float), 256) +
@@ -1219,14 +1260,12 @@ extern "C" int mivq_adc_search(const float* lut, int64_t nq, const uint8_t* code
                                                align_up((size_t)parts_ws * nq * k * sizeof(float), 256));
     // the filtered path (integer-LUT scan + exact re-rank + certificate; the fp32 scan re-runs
     // only the uncertified queries): same results, ~half the LDS traffic per (query, row)
-    const char* force_exact = getenv("MIVQ_ADC_EXACT");  // profiling: the fp32 scan for every query
     const bool filtered = fshape && reinterpret_cast<uintptr_t>(codes) % 16 == 0 &&
-                          reinterpret_cast<uintptr_t>(lut) % 16 == 0 && !(force_exact && atoi(force_exact) != 0);
+                          reinterpret_cast<uintptr_t>(lut) % 16 == 0 && !(flags & MIVQ_ADC_FORCE_EXACT);
     const int* qlist = nullptr;
     const int* qcount = nullptr;
     hipError_t e;
-    const char* nofb = getenv("MIVQ_ADC_NO_FALLBACK");  // tests: certified queries only, the others NaN
-    const bool no_fallback = nofb && atoi(nofb) != 0;
+    const bool no_fallback = (flags & MIVQ_ADC_NO_RERUN) != 0;  // test hook: certified queries only, the others NaN
     if (filtered) {
         const AdcFilteredLayout FL = adc_filtered_layout(nq, n, M, k, exact_bytes);
         unsigned char* ws = static_cast<unsigned char*>(workspace);
@@ -1238,23 +1277,17 @@ extern "C" int mivq_adc_search(const float* lut, int64_t nq, const uint8_t* code
         if (e != hipSuccess) return set_error(MIVQ_ERR_HIP, "adc_search (filtered): %s", hipGetErrorString(e));
         qcount = reinterpret_cast<const int*>(ws + FL.fail);
         qlist = qcount + 1;
-        if (const char* sv = getenv("MIVQ_ADC_STATS"); sv && atoi(sv) != 0) {  // profiling: blocking
-            int cnt = -1;
-            if (hipMemcpyAsync(&cnt, qcount, sizeof(int), hipMemcpyDeviceToHost, st) == hipSuccess &&
-                hipStreamSynchronize(st) == hipSuccess)
-                fprintf(stderr, "mivq_adc_search: %d of %lld queries not certified (re-run on the fp32 scan)\n", cnt,
-                        (long long)nq);
-        }
         if (no_fallback) return MIVQ_OK;
     }
     const int64_t nch = filtered ? nch_fb : nch_exact;
     const int parts = (int)(nch * kScanWaves);
+    const bool sg = filtered && (flags & MIVQ_ADC_SMALL_RERUN_GRID) != 0;
     const int R = (k + 63) / 64;
     switch (R) {
-        case 1: e = launch_scan_r<1>(QB, lut, nq, codes, n, M, ksub, k, id_offset, nch, pd, pi, st, qlist, qcount); break;
-        case 2: e = launch_scan_r<2>(QB, lut, nq, codes, n, M, ksub, k, id_offset, nch, pd, pi, st, qlist, qcount); break;
-        case 3: e = launch_scan_r<3>(QB, lut, nq, codes, n, M, ksub, k, id_offset, nch, pd, pi, st, qlist, qcount); break;
-        default: e = launch_scan_r<4>(QB, lut, nq, codes, n, M, ksub, k, id_offset, nch, pd, pi, st, qlist, qcount); break;
+        case 1: e = launch_scan_r<1>(QB, lut, nq, codes, n, M, ksub, k, id_offset, nch, pd, pi, st, qlist, qcount, sg); break;
+        case 2: e = launch_scan_r<2>(QB, lut, nq, codes, n, M, ksub, k, id_offset, nch, pd, pi, st, qlist, qcount, sg); break;
+        case 3: e = launch_scan_r<3>(QB, lut, nq, codes, n, M, ksub, k, id_offset, nch, pd, pi, st, qlist, qcount, sg); break;
+        default: e = launch_scan_r<4>(QB, lut, nq, codes, n, M, ksub, k, id_offset, nch, pd, pi, st, qlist, qcount, sg); break;
     }
     if (e != hipSuccess) return set_error(MIVQ_ERR_HIP, "adc_scan: %s", hipGetErrorString(e));
     e = launch_topk_merge(pd, pi, parts, nq, k, dists, ids, st, qlist, qcount);

@@ -76,7 +76,8 @@ SIGNATURES = {
     "mivq_extrabitq_rotate": (_c.c_int, [_vp, _i64, _i32, _vp, _i32, _vp, _vp]),
     "mivq_adc_lut": (_c.c_int, [_vp, _i64, _i32, _i32, _i32, _vp, _i32, _vp, _vp]),
     "mivq_adc_search_workspace_bytes": (_sz, [_i64, _i64, _i32, _i32, _i32]),
-    "mivq_adc_search": (_c.c_int, [_vp, _i64, _vp, _i64, _i32, _i32, _i32, _i64, _vp, _sz, _vp, _vp, _vp]),
+    "mivq_adc_search": (_c.c_int, [_vp, _i64, _vp, _i64, _i32, _i32, _i32, _i64, _vp, _sz, _vp, _vp, _c.c_uint32,
+                                   _vp]),
     "mivq_flat_search_workspace_bytes": (_sz, [_i64, _i64, _i32, _i32]),
     "mivq_flat_search": (_c.c_int, [_vp, _i64, _vp, _i64, _i32, _i32, _i32, _i64, _vp, _sz, _vp, _vp, _vp]),
     "mivq_topk_merge": (_c.c_int, [_vp, _vp, _i32, _i64, _i32, _vp, _vp, _vp]),
@@ -93,6 +94,7 @@ SIGNATURES = {
                                      _vp, _sz, _vp, _vp, _vp]),
 }
 
+ABI_VERSION = 2  # MIVQ_ABI_VERSION of include/mivq.h the table above binds
 _lib: Optional[ctypes.CDLL] = None
 _lock = threading.Lock()
 
@@ -108,6 +110,10 @@ def load_library() -> ctypes.CDLL:
                     "`make -C vector-quantization_amd/csrc` (or __graft_entry__.build())"
                 )
             lib = ctypes.CDLL(str(LIB_PATH))
+            lib.mivq_abi_version.restype = ctypes.c_int
+            if lib.mivq_abi_version() != ABI_VERSION:
+                raise RuntimeError(f"{LIB_PATH} has ABI {lib.mivq_abi_version()}, this package binds ABI "
+                                   f"{ABI_VERSION}: rebuild it (make -C vector-quantization_amd/csrc)")
             for name, (res, args) in SIGNATURES.items():
                 fn = getattr(lib, name)
                 fn.restype = res
@@ -491,8 +497,14 @@ def adc_lut(q: torch.Tensor, centroids: torch.Tensor, nbits: int, metric: int = 
     return lut
 
 
+# mivq_adc_search flags (include/mivq.h): the product path always passes ADC_AUTO; the others are
+# diagnostics (FORCE_EXACT: same results on the fp32 scan) and test hooks (NO_RERUN leaves the
+# queries the filter cannot certify NaN)
+ADC_AUTO, ADC_FORCE_EXACT, ADC_NO_RERUN, ADC_SMALL_RERUN_GRID = 0, 1, 2, 4
+
+
 def adc_search(lut: torch.Tensor, codes_u8: torch.Tensor, k: int, nbits: int,
-               id_offset: int = 0) -> Tuple[torch.Tensor, torch.Tensor]:
+               id_offset: int = 0, flags: int = ADC_AUTO) -> Tuple[torch.Tensor, torch.Tensor]:
     """Returns (dists f32 (nq, k), ids int32 (nq, k) holding uint32 bit patterns)."""
     _check(lut, "lut", torch.float32, 3)
     _check(codes_u8, "codes", torch.uint8, 2)
@@ -505,7 +517,7 @@ def adc_search(lut: torch.Tensor, codes_u8: torch.Tensor, k: int, nbits: int,
     nb = load_library().mivq_adc_search_workspace_bytes(nq, n, M, nbits, k)
     ws = workspace(nb, lut.device)
     _call("mivq_adc_search", _ptr(lut), nq, _ptr(codes_u8), n, M, nbits, k, id_offset, _ptr(ws), ws.numel(),
-          _ptr(dists), _ptr(ids), _stream())
+          _ptr(dists), _ptr(ids), flags, _stream())
     return dists, ids
 
 

@@ -72,10 +72,28 @@ def _resolve_path(dataset: str, data_path: Optional[str], cache_dir: str) -> Pat
                             f"or place {dataset}.npy / .fvecs under {root} (or set VQ_DATA_DIR)")
 
 
-def _batch_distortion(model, xb: torch.Tensor, codes) -> float:
-    """compute_distortion (metrics/distortion.py:4-6) on the device-resident batch."""
+def _batch_distortion(model, xb: torch.Tensor, codes) -> torch.Tensor:
+    """compute_distortion (metrics/distortion.py:4-6) on the device-resident batch (a 0-d fp64
+    device tensor: the caller collects them without a sync per batch)."""
     rec = model.decompress(codes)
-    return float(((xb.double() - rec.double()) ** 2).sum(1).mean())
+    return ((xb.double() - rec.double()) ** 2).sum(1).mean()
+
+
+# Stream batches per device encode call.  Upstream's loop calls compress once per 10,000-row
+# batch (streaming_sweep.py:153-185); on the GPU a 10k-row call is launch- and prologue-bound
+# (39 rows per filter workgroup), so consecutive batches of a rank's run go to the device
+# together, ~2^20 rows per call (capped at 4 GiB of fp32 rows), and each batch's distortion is
+# then computed from its own rows and codes exactly as before: codes are row-independent and
+# the per-batch terms are the same tensors of the same shapes, so the logged row does not
+# depend on the grouping (or on the number of ranks).
+CALL_ROWS = 1 << 20
+CALL_BYTES = 4 << 30
+
+
+def batches_per_call(batch_size: int, dim: int) -> int:
+    by_rows = max(1, CALL_ROWS // max(1, batch_size))
+    by_bytes = max(1, CALL_BYTES // max(1, batch_size * dim * 4))
+    return min(by_rows, by_bytes)
 
 
 def batch_plan(n_total: int, batch_size: int, max_batches: Optional[int], rank: int = 0,
@@ -192,18 +210,30 @@ def streaming_sweep(
     starts, (b0, b1) = batch_plan(n_total, batch_size, max_batches, info.rank, info.world)
     part = np.zeros((len(starts), 2), dtype=np.float64)  # per batch: mse * count, count
     timers = []
-    for b in range(b0, b1):
-        s = starts[b]
-        xb = _arrays.to_device(np.ascontiguousarray(stream[s:s + batch_size], dtype=np.float32))
+    per_call = batches_per_call(batch_size, dim)
+    mse_dev = []  # (batch index, 0-d fp64 device tensor)
+    for g0 in range(b0, b1, per_call):
+        g1 = min(b1, g0 + per_call)
+        r0, r1 = starts[g0], min(n_total, starts[g1 - 1] + batch_size)
+        xg = _arrays.to_device(np.ascontiguousarray(stream[r0:r1], dtype=np.float32))
         ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
         ev[0].record()
-        codes = model.compress(xb)
+        codes = model.compress(xg)  # one device call for the batches g0 .. g1-1
         ev[1].record()
         timers.append(ev)
-        part[b] = (_batch_distortion(model, xb, codes) * xb.shape[0], xb.shape[0])  # weighted, as upstream
-        if head and (b - b0 + 1) % 100 == 0:
-            say(f"  Compressed {b - b0 + 1} batches on rank 0 ({int(part[b0:b + 1, 1].sum()):,} vectors)")
+        for b in range(g0, g1):
+            s, e = starts[b] - r0, min(n_total, starts[b] + batch_size) - r0
+            # the batch's codes as a fresh allocation, as a per-batch call returned them
+            mse_dev.append((b, _batch_distortion(model, xg[s:e], codes[s:e].clone())))
+            part[b, 1] = e - s
+            if head and (b - b0 + 1) % 100 == 0:
+                say(f"  Compressed {b - b0 + 1} batches on rank 0 ({int(part[b0:b + 1, 1].sum()):,} vectors)")
+        del xg, codes
     torch.cuda.synchronize()
+    if mse_dev:
+        vals = torch.stack([t for _, t in mse_dev]).cpu().numpy()
+        for (b, _), v in zip(mse_dev, vals):
+            part[b, 0] = float(v) * part[b, 1]  # weighted, as upstream
     enc_s = sum(e0.elapsed_time(e1) for e0, e1 in timers) * 1e-3
     ratio = model.get_compression_ratio(training)
     code_bytes = 4 * dim / ratio  # bytes per encoded vector (every ratio is 4 D / code bytes)

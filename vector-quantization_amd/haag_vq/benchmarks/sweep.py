@@ -107,7 +107,9 @@ def sweep(
     world = launched_world()
     if world > 1 and gpus != world:
         raise ValueError(f"sweep: --gpus {gpus} but WORLD_SIZE={world}")
-    info = init_rank(device)
+    # configurations are dealt by RANK / WORLD_SIZE alone: no process group (no collective
+    # to wait in while another rank runs a longer configuration)
+    info = init_rank(device, collectives=False)
 
     if codebooks_dir is None:
         codebooks_dir = os.getenv("CODEBOOKS_DIR")

@@ -98,9 +98,14 @@ def polar_factor(G: torch.Tensor, tol: float = 1e-13, max_iter: int = 60, info: 
     vector -- cannot rule that out).  It doubles the digits once every singular value is near 1,
     and stops at ||Q^T Q - I||_F < tol sqrt(d) or once that error stalls at the fp64 rounding
     floor of the GEMMs.  A G the iteration cannot orthogonalise (rank deficient, or not
-    converged within max_iter: condition numbers far beyond 1e8) falls back to the SVD; a
+    converged within max_iter, or singular values below ~1e-6 of the top, whose growth the
+    trace test below cannot see in fp64) falls back to the SVD; a
     rank-deficient G is recognised by its error stalling above 1e-8 (the zero singular values
-    stay at zero, ||Q^T Q - I|| levels off at sqrt(#zeros)) for 4 steps, not after max_iter.
+    stay at zero, ||Q^T Q - I|| levels off at sqrt(#zeros)) for 4 steps while trace(Q^T Q) =
+    sum sigma^2 stays put, not after max_iter.  Small but non-zero singular values (a tail of
+    low-variance directions, e.g. 1e-3 of the top) also hold the error near sqrt(#small) for a
+    while, but they grow by 1.5x per step, so the trace moves and the iteration goes on
+    (the error test alone sent such G to the SVD).
     ``info`` (optional dict) receives {"path": "newton-schulz" | "svd", "iters": steps}."""
     d = G.shape[0]
     I = torch.eye(d, dtype=torch.float64, device=G.device)
@@ -108,20 +113,22 @@ def polar_factor(G: torch.Tensor, tol: float = 1e-13, max_iter: int = 60, info: 
     bound = min(float(G.norm()), float(GtG.abs().sum(dim=1).max()) ** 0.5)
     if bound > 0.0 and bound < float("inf"):
         Q = G / bound
-        prev, stall = float("inf"), 0
+        prev, prev_tr, stall = float("inf"), float("nan"), 0
         for it in range(max_iter):
             T = _mm(Q.T, Q)
             err = float((T - I).norm())
+            tr = float(T.diagonal().sum())
             if err < tol * d ** 0.5 or (err < 1e-8 and err > 0.25 * prev):
                 if info is not None:
                     info.update(path="newton-schulz", iters=it)
                 return Q  # converged (quadratic phase stalled: the rounding floor)
             if not err < 1e3:  # non-finite
                 break
-            stall = stall + 1 if err >= 0.999 * prev else 0
+            # levelled off above 1e-8 with sum sigma^2 not moving: zero singular values
+            stall = stall + 1 if err >= 0.999 * prev and abs(tr - prev_tr) <= 1e-12 * d else 0
             if stall >= 4:
-                break  # levelled off above 1e-8: zero singular values
-            prev = err
+                break
+            prev, prev_tr = err, tr
             Q = 1.5 * Q - 0.5 * _mm(Q, T)
     if info is not None:
         info.update(path="svd", iters=it + 1 if bound > 0.0 and bound < float("inf") else 0)

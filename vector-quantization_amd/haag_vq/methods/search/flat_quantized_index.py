@@ -51,7 +51,12 @@ def search_codes(model: BaseQuantizer, codes, Q, k: int, metric: str = "l2",
     cd = cd.to(_arrays.device())
     if k > MAX_KERNEL_K:
         d, i = _search_large_k(model, cd, Qd, k, mt)
-        return d, (i.to(torch.int64) + id_offset).to(torch.int32) if id_offset else i
+        if id_offset:
+            # ids are uint32 bit patterns in int32: mask before adding, and keep the
+            # 0xFFFFFFFF sentinel as it is
+            g = ((i.to(torch.int64) & 0xFFFFFFFF) + id_offset) & 0xFFFFFFFF
+            i = torch.where(i == -1, i, (g - (g >= 2 ** 31).to(torch.int64) * 2 ** 32).to(torch.int32))
+        return d, i
     if isinstance(model, (ProductQuantizer, OptimizedProductQuantizer)):
         pq = model if isinstance(model, ProductQuantizer) else model.inner
         if isinstance(model, OptimizedProductQuantizer):

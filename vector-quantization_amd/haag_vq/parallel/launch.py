@@ -16,6 +16,7 @@ import socket
 import subprocess
 import sys
 from dataclasses import dataclass
+from datetime import timedelta
 from typing import List, Optional
 
 import torch
@@ -66,9 +67,17 @@ def launch_ranks(gpus: int, module_args: List[str], extra_env: Optional[dict] = 
     return subprocess.call(cmd, env=env)
 
 
-def init_rank(device_index: Optional[int] = None) -> RankInfo:
+# Ranks of the CLI callers wait in collectives while another rank trains or runs a longer
+# configuration (streaming-sweep: ranks 1..N-1 wait in the quantizer broadcast while rank 0 fits
+# on 1M rows): the default 10-minute watchdog would abort them
+RANK_TIMEOUT = timedelta(hours=12)
+
+
+def init_rank(device_index: Optional[int] = None, collectives: bool = True) -> RankInfo:
     """Joins the process group of torch.distributed.run (no-op at world size 1).  A single
-    process runs on ``device_index`` (default: the current device)."""
+    process runs on ``device_index`` (default: the current device).  ``collectives=False``
+    (``sweep --gpus N``, which only deals configurations by RANK / WORLD_SIZE) picks the rank's
+    device and opens no process group at all."""
     world = launched_world()
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
@@ -82,12 +91,12 @@ def init_rank(device_index: Optional[int] = None) -> RankInfo:
         device = torch.device("cuda", idx)
         torch.cuda.set_device(device)
     backend = None
-    if world > 1:
+    if world > 1 and collectives:
         backend = os.environ.get("VQ_DIST_BACKEND") or ("nccl" if has_gpu else "gloo")
         if backend == "nccl":
-            dist.init_process_group("nccl", device_id=device)
+            dist.init_process_group("nccl", device_id=device, timeout=RANK_TIMEOUT)
         else:
-            dist.init_process_group(backend)
+            dist.init_process_group(backend, timeout=RANK_TIMEOUT)
     return RankInfo(rank, world, local, backend, device)
 
 

@@ -63,6 +63,34 @@ MFMA_F32_PEAK_TFS = 157.3      # dense fp32 matrix peak (same table)
 MFMA_F16_PEAK_TFS = 2516.6     # dense f16/bf16 matrix peak = 16 x fp32 (same table)
 MFMA_F64_PEAK_TFS = 78.6       # dense fp64 matrix peak (MI355X spec; not in the guide's table)
 LDS_PEAK_GBS = 256 * 256 * 2.4  # 256 CUs x 256 B/clk (ds_read_b128) x 2.4 GHz = 157 TB/s
+# The filtered ADC scan (adc_qscan_kernel) is VALU-issue bound (its LDS reads are
+# conflict-free since round 6 and PMC shows the VALU pipe saturated, profiles/r06_s1/pmc_*).
+# Its roofline is the chip's VALU issue rate for its instruction mix: the static count of one
+# wave-step (64 rows x 16 queries) of the built kernel, split by encoding (tools/isa_qscan.py,
+# checked against the library by tests/test_abi.py) ...
+QSCAN_VALU_PER_STEP = {16: {"valu_32bit": 48, "valu_64bit": 122}, 32: {"valu_32bit": 81, "valu_64bit": 232}}
+# ... priced at the issue rates tools/probes/valu_rate.hip measured with 4 waves per SIMD on every
+# CU (chip wave-instructions/s under that load; profiles/r06_s5/valu_rate.log): 32-bit-encoded
+# VALU (v_add_u32_e32) 0.881e12, 64-bit-encoded VALU (v_perm_b32 / v_med3_u32 / v_lshl_or_b32,
+# all equal) 0.577e12
+VALU_RATE_32BIT = 0.881e12
+VALU_RATE_64BIT = 0.577e12
+
+
+def qscan_valu_roofline(nq, n, M, seconds):
+    """VALU issue roofline of the integer scan: achieved = its VALU wave-instructions (static count
+    per wave-step x wave-steps) / the timed search; peak = the mix-weighted probe rate.  The timed
+    region is the whole mivq_adc_search (table prep, rerank, re-run included), so this is a lower
+    bound of the scan's own rate."""
+    v = QSCAN_VALU_PER_STEP.get(M)
+    if v is None:
+        return None
+    steps = -(-nq // 16) * (n / 64.0)  # wave-steps: query blocks x 64-row groups
+    instr = steps * (v["valu_32bit"] + v["valu_64bit"])
+    peak = (v["valu_32bit"] + v["valu_64bit"]) / (v["valu_32bit"] / VALU_RATE_32BIT + v["valu_64bit"] / VALU_RATE_64BIT)
+    return {"achieved": instr / seconds / 1e9, "peak": peak / 1e9, "unit": "G VALU wave-instructions/s",
+            "frac": instr / seconds / peak, "valu_per_wave_step": v,
+            "valu_instructions_per_search": instr}
 # rigorous relative bound on a canonical fp32 score difference (oracle header): 2 (2 g_96 + u)
 CLEAR_GAP = 3e-5
 
@@ -290,7 +318,7 @@ def cpu_baseline(X, C, O, target_s):
 
 
 # ------------------------------------------------------------------------- ADC
-def adc_leg(X, C, codes, a, rank, world, dev, Q, k, gt_queries, reps=3, cpu=True):
+def adc_leg(X, C, codes, a, rank, world, dev, Q, k, gt_queries, reps=10, cpu=True):
     """Sharded ADC search + its roofline + the reference's decode-then-exact ranking on the
     same codes (+ the oracle's ADC on the host cores at N = 1)."""
     nbits = 8
@@ -317,23 +345,23 @@ def adc_leg(X, C, codes, a, rank, world, dev, Q, k, gt_queries, reps=3, cpu=True
     gt = gi.cpu().numpy().view(np.uint32)
     dec = di.cpu().numpy().view(np.uint32)
     rec = lambda ref, x: float(np.mean([len(set(ref[j]) & set(x[j])) / k for j in range(gq)]))  # noqa: E731
-    lds_bytes = nq * n * M * 4  # one f32 LUT entry per (query, row, subspace)
+    vr = qscan_valu_roofline(nq, n, M, scan_ms * 1e-3)
     out = {"qps": nq / wall, "nq": nq, "k": k, "n_total": n * world, "ms_per_batch": wall * 1e3,
            f"recall@{k}": rec(gt, got), "recall_queries": gq,
            f"recall@{k}_decode_exact": rec(gt, dec), "topk_agreement_adc_vs_decode_exact": rec(dec, got),
            "gt": "exact L2 top-k over the raw vectors (mivq_flat_search, sharded + merged)",
-           "roofline": {"bound": "lds", "kernel": "mivq_adc_search (per rank: qstats + qtab + adc_qscan_kernel + "
-                                                   "adc_rerank_kernel + fp32 re-run of uncertified queries)",
-                        "achieved": lds_bytes / (scan_ms * 1e-3) / 1e9, "peak": LDS_PEAK_GBS, "unit": "GB/s",
-                        "frac": lds_bytes / (scan_ms * 1e-3) / 1e9 / LDS_PEAK_GBS, "scan_ms": scan_ms,
-                        "lds_bytes_per_query_row": M * 4,
-                        # the bytes the integer scan actually reads: one byte per (query, row, subspace)
-                        "lds_bytes_read_frac": nq * n * M / (scan_ms * 1e-3) / 1e9 / LDS_PEAK_GBS,
-                        "note": "algorithmic bytes = one fp32 LUT entry per (query, row, subspace), the canonical "
-                                "ADC's table reads (SURVEY 8d); the filtered search (DESIGN 3.3) scans 1-B 6-bit "
-                                "entries, 16 queries per 16-B read, so frac can exceed 1; its own LDS reads are "
-                                "lds_bytes_read_frac of the peak and its scan is bound by VALU issue (177 VALU per "
-                                "row and 16 queries)"}}
+           "roofline": dict({"bound": "valu", "kernel": "mivq_adc_search (per rank: adc_qstats + adc_qtab + adc_qscan_kernel "
+                                                        "+ adc_rerank_kernel + fp32 re-run of uncertified queries)",
+                             "scan_ms": scan_ms,
+                             # the integer scan's own LDS reads (one byte per (query, row, subspace),
+                             # conflict-free since round 6) against the LDS peak, for reference
+                             "lds_bytes_read_frac": nq * n * M / (scan_ms * 1e-3) / 1e9 / LDS_PEAK_GBS,
+                             "note": "VALU-issue roofline of the integer scan (bench.py qscan_valu_roofline, "
+                                     "DESIGN 3.3): static VALU per wave-step of the built kernel priced at the "
+                                     "measured issue rates; the timed region is the whole search"},
+                            **(vr or {"bound": "lds", "achieved": nq * n * M * 4 / (scan_ms * 1e-3) / 1e9,
+                                      "peak": LDS_PEAK_GBS, "unit": "GB/s (fp32 LUT entries, the fp32 scan)",
+                                      "frac": nq * n * M * 4 / (scan_ms * 1e-3) / 1e9 / LDS_PEAK_GBS}))}
     if cpu and rank == 0 and world == 1:
         O = _oracle()
         # a bounded sample: ~1 s wall on the box's 16 threads (~16 thread-s)

@@ -103,3 +103,22 @@ def test_adc_search_workspace_bounded():
     assert 0 < nb < 800 * 2 ** 20, nb
     nb = lib.mivq_adc_search_workspace_bytes(100_000, 10_000_000, 16, 8, 32)
     assert 0 < nb < 3 * 2 ** 30, nb
+
+
+def test_qscan_valu_counts_match_bench():
+    """bench.py prices the filtered ADC scan's roofline from the static VALU count of one
+    wave-step of adc_qscan_kernel (QSCAN_VALU_PER_STEP); that count must be the built library's."""
+    import sys
+
+    if not Path("/opt/rocm/lib/llvm/bin/llvm-objdump").exists():
+        pytest.skip("ROCm LLVM tools not present")
+    sys.path.insert(0, str(ROOT / "tools"))
+    sys.path.insert(0, str(ROOT))
+    import bench
+    import isa_qscan
+    from haag_vq import _native
+
+    got = isa_qscan.count(Path(_native.LIB_PATH))
+    for M, v in bench.QSCAN_VALU_PER_STEP.items():
+        assert got[str(M)]["valu_32bit"] == v["valu_32bit"] and got[str(M)]["valu_64bit"] == v["valu_64bit"], got
+        assert got[str(M)]["ds_read_b128"] == M  # one 16-B table read per subspace

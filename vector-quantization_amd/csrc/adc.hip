@@ -20,6 +20,7 @@ namespace mivq {
 namespace {
 
 typedef float v4f __attribute__((ext_vector_type(4)));  // native vector: HIP's float4 struct copies can defeat SROA
+typedef float float2v __attribute__((ext_vector_type(2)));
 constexpr int kScanWaves = 16;  // waves per scan workgroup (adc and flat)
 
 // L2: lut[q][m][k] = fmaf chain over t of (q_t - c_t)^2;  IP: -(fmaf chain of q_t * c_t)
@@ -90,6 +91,66 @@ __global__ __launch_bounds__(256) void adc_lut_kernel(const float* __restrict__ 
 #pragma unroll
     for (int qq = 0; qq < kLutQ; ++qq)
         if (qq < nqb) lut[((q0 + qq) * M + m) * ksub + k] = l2 ? acc[qq] : -acc[qq];
+}
+
+// ksub = 256, dsub % 4 == 0, C 16-B aligned (round 6): packed fp32.  Grid (M, ceil(nq / 8)),
+// block 128: thread k takes centroids k and k + 128 as the two halves of v_pk_add_f32 /
+// v_pk_fma_f32 (both chains exactly the scalar ones: the same sub, then fma, over t ascending),
+// and the 8 queries' values come through the scalar cache as the broadcast operand -- no LDS,
+// so no packed instruction reads an LDS-loaded register.  Half the VALU of the
+// scalar kernel, and no LDS reads at all.
+constexpr int kLutPkQ = 8;
+template <bool L2>
+__global__ __launch_bounds__(128) void adc_lut_pk_kernel(const float* __restrict__ q, int64_t nq, int d, int M,
+                                                          int dsub, const float* __restrict__ C,
+                                                          float* __restrict__ lut) {
+    const int m = blockIdx.x;
+    const int64_t q0 = (int64_t)blockIdx.y * kLutPkQ;
+    const int nqb = (int)min<int64_t>(kLutPkQ, nq - q0);
+    const int k = threadIdx.x;
+    const float* ca = C + ((int64_t)m * 256 + k) * dsub;
+    const float* cb = ca + (int64_t)128 * dsub;
+    const float* qr[kLutPkQ];
+#pragma unroll
+    for (int qq = 0; qq < kLutPkQ; ++qq) qr[qq] = q + (q0 + min(qq, nqb - 1)) * d + (int64_t)m * dsub;  // in range
+    float2v acc[kLutPkQ];
+#pragma unroll
+    for (int qq = 0; qq < kLutPkQ; ++qq) acc[qq] = (float2v){0.0f, 0.0f};
+    v4f a = *reinterpret_cast<const v4f*>(ca), b = *reinterpret_cast<const v4f*>(cb);
+#ifndef MIVQ_LUT_UNROLL
+#define MIVQ_LUT_UNROLL 1
+#endif
+#pragma unroll MIVQ_LUT_UNROLL
+    for (int t0 = 0; t0 < dsub; t0 += 4) {
+        const bool more = t0 + 4 < dsub;
+        const v4f an = more ? *reinterpret_cast<const v4f*>(ca + t0 + 4) : a;
+        const v4f bn = more ? *reinterpret_cast<const v4f*>(cb + t0 + 4) : b;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const float2v cc = {a[j], b[j]};
+#pragma unroll
+            for (int qq = 0; qq < kLutPkQ; ++qq) {
+                const float qv = qr[qq][t0 + j];
+                const float2v qq2 = {qv, qv};
+                if constexpr (L2) {
+                    const float2v df = qq2 - cc;
+                    acc[qq] = __builtin_elementwise_fma(df, df, acc[qq]);
+                } else {
+                    acc[qq] = __builtin_elementwise_fma(qq2, cc, acc[qq]);
+                }
+            }
+        }
+        a = an;
+        b = bn;
+    }
+#pragma unroll
+    for (int qq = 0; qq < kLutPkQ; ++qq) {
+        if (qq < nqb) {
+            float* o = lut + ((q0 + qq) * M + m) * 256;
+            o[k] = L2 ? acc[qq].x : -acc[qq].x;
+            o[k + 128] = L2 ? acc[qq].y : -acc[qq].y;
+        }
+    }
 }
 
 // Table group mk (= m*ksub + code) holds the QB queries' entries of (m, code) side by side.
@@ -623,6 +684,8 @@ __global__ __launch_bounds__(256) void adc_qtab_kernel(const float* __restrict__
     }
 }
 
+constexpr int kQB = 16;  // queries per integer-table block
+
 // grid (nchunks, ceil(nq / 16)), block kScanWaves waves (the fp32 scan's structure): the byte
 // tables of 16 queries in LDS (M * 4 KiB), M = 16 MC, each lane one row per wave-step with its
 // code row loaded a step ahead.  No wave-level list during the scan: every lane keeps, per
@@ -634,7 +697,6 @@ __global__ __launch_bounds__(256) void adc_qtab_kernel(const float* __restrict__
 // row of the part that is not listed has S >= B (a lane's other rows are >= its last kept
 // key, a dropped candidate is >= T).  (The round-5 first cut kept wave-resident exact lists
 // updated by ballot + shuffle inserts: those inserts were most of its LDS instructions.)
-constexpr int kQB = 16;  // queries per integer-table block
 
 __device__ __forceinline__ uint32_t umed3(uint32_t a, uint32_t b, uint32_t c) {
     uint32_t r;
@@ -699,6 +761,30 @@ __global__ __launch_bounds__(kScanWaves * 64) void adc_qscan_kernel(
 #pragma unroll
     for (int b = 0; b < 4; ++b)  // byte0 <- mo byte b (S1), byte1 <- code byte (b + rb) % 4 (S0), bytes 2, 3 <- 0
         psel[b] = (uint32_t)b | ((4u + ((b + rb) & 3u)) << 8) | 0x0C0C0000u;
+#ifndef MIVQ_QSCAN_BUF
+#define MIVQ_QSCAN_BUF 1
+#endif
+    // M = 16 (MC = 1): the code row's dwords come rotated by rd straight from memory: four dword buffer loads per
+    // 16-B half with per-lane offsets fixed for the whole kernel (the lane's row and rotation)
+    // and the wave-step in the scalar soffset, range-checked over the chunk (rows past it read
+    // zeros), so neither the rotation nor the row address costs VALU.  (M = 32: the select
+    // rotation below; eight such loads per row spilled there.)
+    constexpr bool kBuf = MIVQ_QSCAN_BUF && MC == 1;
+    const __amdgpu_buffer_rsrc_t crs = __builtin_amdgcn_make_buffer_rsrc(
+        (void*)(codes + rbeg * (16 * MC)), 0, (int)(max<int64_t>(0, rend - rbeg) * (16 * MC)), 0x00020000);
+    int voffc[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) voffc[i] = (wv * 64 + lane) * (16 * MC) + 4 * (int)((i + rd) & 3u);
+    auto fetchb = [&](int64_t base) __attribute__((always_inline)) {
+        const int so = (int)(base - rbeg) * (16 * MC);
+#pragma unroll
+        for (int c = 0; c < MC; ++c) {
+            cw[c].x = __builtin_amdgcn_raw_buffer_load_b32(crs, voffc[0], so + 16 * c, 0);
+            cw[c].y = __builtin_amdgcn_raw_buffer_load_b32(crs, voffc[1], so + 16 * c, 0);
+            cw[c].z = __builtin_amdgcn_raw_buffer_load_b32(crs, voffc[2], so + 16 * c, 0);
+            cw[c].w = __builtin_amdgcn_raw_buffer_load_b32(crs, voffc[3], so + 16 * c, 0);
+        }
+    };
     // the code row's dwords rotated by rd within each 16-B half (two select levels)
     auto rot = [&](uint4 w) __attribute__((always_inline)) {
         const bool r1 = (rd & 1u) != 0u, r2 = (rd & 2u) != 0u;
@@ -710,7 +796,8 @@ __global__ __launch_bounds__(kScanWaves * 64) void adc_qscan_kernel(
     constexpr int UNP = 1 << (8 - kAdcBits);
     static_assert(UNP == 1 || UNP == 2 || UNP == 4 || UNP == 8, "entry bits");
     const int64_t first = rbeg + (int64_t)wv * 64;
-    fetch(first + lane);
+    if constexpr (kBuf) fetchb(rbeg);
+    else fetch(first + lane);
     uint32_t step = 0;
     for (int64_t base = first; base < rend; base += kScanWaves * 64, ++step) {
         const int64_t row = base + lane;
@@ -720,11 +807,12 @@ __global__ __launch_bounds__(kScanWaves * 64) void adc_qscan_kernel(
         uint4 cur[MC];
 #pragma unroll
         for (int c = 0; c < MC; ++c) cur[c] = cw[c];
-        fetch(row + kScanWaves * 64);
+        if constexpr (kBuf) fetchb(base - (int64_t)wv * 64 + kScanWaves * 64);
+        else fetch(row + kScanWaves * 64);
         uint32_t wq[4 * MC];
 #pragma unroll
         for (int c = 0; c < MC; ++c) {
-            cur[c] = rot(cur[c]);
+            if constexpr (!kBuf) cur[c] = rot(cur[c]);
             wq[4 * c + 0] = cur[c].x; wq[4 * c + 1] = cur[c].y;
             wq[4 * c + 2] = cur[c].z; wq[4 * c + 3] = cur[c].w;
         }
@@ -780,8 +868,12 @@ __global__ __launch_bounds__(kScanWaves * 64) void adc_qscan_kernel(
         uint32_t sv[kLaneKeys];
 #pragma unroll
         for (int t = 0; t < kLaneKeys; ++t) sv[t] = mk[t][qq] >> 16;  // 0xFFFF: no candidate
-        // T: the largest t in [0, 0xFFFF] with #{candidates with S < t} <= k1
-        uint32_t lo = 0, hi = 0xFFFF;  // keys of rows past the chunk have S = 0xFFFF: never candidates
+        // T: the largest t in [0, 0xFFFF] with #{candidates with S < t} <= k1.  Real sums are at
+        // most kSMax = M * QMAX (keys of rows past the chunk have S = 0xFFFF: never candidates),
+        // so the search runs over [0, kSMax + 1] (11 steps at M = 16 instead of 16) and a result
+        // of kSMax + 1 (every kept key listed) stands for 0xFFFF
+        constexpr uint32_t kSMax = (uint32_t)M * ((1u << kAdcBits) - 1u);
+        uint32_t lo = 0, hi = kSMax + 1;
         while (lo < hi) {  // wave-uniform
             const uint32_t mid = (lo + hi + 1) >> 1;
             int cnt = 0;
@@ -789,12 +881,11 @@ __global__ __launch_bounds__(kScanWaves * 64) void adc_qscan_kernel(
             for (int t = 0; t < kLaneKeys; ++t) cnt += __popcll(__ballot(sv[t] < mid));
             if (cnt <= k1) lo = mid; else hi = mid - 1;
         }
-        const uint32_t T = lo;
-        uint32_t blo = 0, bhi = 0xFFFF;  // min over lanes of the last kept key's S
-        while (blo < bhi) {
-            const uint32_t mid = (blo + bhi + 1) >> 1;
-            if (__ballot(sv[kLaneKeys - 1] < mid) == 0ull) blo = mid; else bhi = mid - 1;
-        }
+        const uint32_t T = lo > kSMax ? 0xFFFFu : lo;
+        // min over lanes of the last kept key's S: a wave reduction, not a ballot search
+        uint32_t blo = sv[kLaneKeys - 1];
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) blo = min(blo, (uint32_t)__shfl_xor((int)blo, o));
         const uint32_t B = min(T, blo);
         float* od = part_d + (part * nq + q0 + qq) * k1;
         uint32_t* oi = part_i + (part * nq + q0 + qq) * k1;
@@ -856,20 +947,37 @@ __global__ __launch_bounds__(256) void adc_rerank_kernel(const float* __restrict
         __builtin_amdgcn_wave_barrier();
     }
     const int64_t total = (int64_t)parts * k1;
-    for (int64_t e0 = 0; e0 < total; e0 += 64) {
+    // three-stage pipeline over the list in steps of 64 entries (round 6): the ids two steps
+    // ahead and the code rows (which need those ids) one step ahead are in flight while a step
+    // is evaluated, instead of an id load -> row gather -> lookups round trip per step
+    auto ld_id = [&](int64_t e0) __attribute__((always_inline)) {
         const int64_t e = e0 + lane;
         uint32_t id = kNoId;
         if (e < total) {
             const int64_t p = e / k1, j = e - p * k1;
             id = pi[(p * nq + qi) * k1 + j];
         }
+        return id;
+    };
+    auto ld_row = [&](uint32_t id, uint4 (&cw)[MC]) __attribute__((always_inline)) {
+        const uint4* cr = reinterpret_cast<const uint4*>(codes + ((int64_t)(id != kNoId ? id : (uint32_t)id_offset) - id_offset) * M);
+#pragma unroll
+        for (int c = 0; c < MC; ++c) cw[c] = id != kNoId ? cr[c] : make_uint4(0u, 0u, 0u, 0u);
+    };
+    uint32_t id_cur = ld_id(0), id_nxt = ld_id(64);
+    uint4 cw_cur[MC];
+    ld_row(id_cur, cw_cur);
+    for (int64_t e0 = 0; e0 < total; e0 += 64) {
+        const uint32_t id_far = ld_id(e0 + 128);
+        uint4 cw_nxt[MC];
+        ld_row(id_nxt, cw_nxt);
+        const uint32_t id = id_cur;
         const bool valid = id != kNoId;
         float dv = INFINITY;
         if (valid) {
-            const uint4* cr = reinterpret_cast<const uint4*>(codes + ((int64_t)id - id_offset) * M);
             uint4 cw[MC];
 #pragma unroll
-            for (int c = 0; c < MC; ++c) cw[c] = cr[c];
+            for (int c = 0; c < MC; ++c) cw[c] = cw_cur[c];
             float t[M];
 #pragma unroll
             for (int c = 0; c < MC; ++c) {
@@ -884,6 +992,10 @@ __global__ __launch_bounds__(256) void adc_rerank_kernel(const float* __restrict
             if (dv != dv) dv = INFINITY;
         }
         top.offer(valid, dv, id, k, lane, thr_d, thr_i);
+        id_cur = id_nxt;
+        id_nxt = id_far;
+#pragma unroll
+        for (int c = 0; c < MC; ++c) cw_cur[c] = cw_nxt[c];
     }
     // certificate: every part's bound B (its unlisted rows have S >= B) must put them above E_k
     bool ok = !st.bad;
@@ -1088,6 +1200,8 @@ hipError_t launch_filtered(int M, const float* lut, int64_t nq, const uint8_t* c
     int* fail_list = fail_count + 1;
     hipError_t e = hipMemsetAsync(fail_count, 0, sizeof(int), st);
     if (e != hipSuccess) return e;
+    // (round 6: the two launches fused into one workgroup per 16-query block measured slower --
+    // 0.422 vs 0.406 ms per 1000 x 1M search: 63 workgroups leave most CUs idle; profiles/r06_s5)
     hipLaunchKernelGGL(adc_qstats_kernel, dim3((unsigned)nq), dim3(256), 0, st, lut, nq, M, mins, qs);
     const dim3 tgrid((unsigned)ceil_div(nq, QB), (unsigned)M);
     if (QB == 16)
@@ -1202,6 +1316,19 @@ extern "C" int mivq_adc_lut(const float* q, int64_t nq, int32_t d, int32_t M, in
     if (nq == 0) return MIVQ_OK;
     MIVQ_REQUIRE(q && centroids && lut, MIVQ_ERR_INVALID, "adc_lut: null pointer");
     const int ksub = 1 << nbits;
+#ifndef MIVQ_LUT_PK
+#define MIVQ_LUT_PK 1
+#endif
+    if (MIVQ_LUT_PK && ksub == 256 && (d / M) % 4 == 0 && reinterpret_cast<uintptr_t>(centroids) % 16 == 0) {
+        const dim3 grid((unsigned)M, (unsigned)ceil_div(nq, kLutPkQ));
+        if (metric == MIVQ_METRIC_L2)
+            hipLaunchKernelGGL(adc_lut_pk_kernel<true>, grid, dim3(128), 0, as_stream(stream), q, nq, d, M, d / M,
+                               centroids, lut);
+        else
+            hipLaunchKernelGGL(adc_lut_pk_kernel<false>, grid, dim3(128), 0, as_stream(stream), q, nq, d, M, d / M,
+                               centroids, lut);
+        return check_launch("adc_lut");
+    }
     const size_t smem = (size_t)kLutQ * (d / M) * sizeof(float);
     MIVQ_REQUIRE(smem <= 64 * 1024, MIVQ_ERR_UNSUPPORTED, "adc_lut: dsub=%d too large", d / M);
     hipLaunchKernelGGL(adc_lut_kernel, dim3((unsigned)M, (unsigned)ceil_div(nq, kLutQ)), dim3(256), smem,

@@ -440,12 +440,37 @@ __global__ __launch_bounds__(256) void topk_seg_kernel(const float* __restrict__
     top.init();
     float thr_d = INFINITY;
     uint32_t thr_i = kNoId;
-    for (int64_t j0 = c0; j0 < c1; j0 += 64) {
-        const int64_t j = j0 + lane;
-        const bool valid = j < c1;
-        float v = valid ? dr[j] : INFINITY;
-        if (v != v) v = INFINITY;
-        top.offer(valid, v, (uint32_t)(base + j), k, lane, thr_d, thr_i);
+    // 256 columns per step, four coalesced dword loads per lane, the next step's in flight while
+    // this one is screened; a step none of whose values beats the current k-th element costs one
+    // ballot (round 6: the loop was one dependent 4-B load per 64 columns).  The list is exact
+    // in (dist, id), so the order the candidates are offered in does not change it.
+    float v[4], vn[4];
+    auto ldv = [&](int64_t j0, float (&dst)[4]) __attribute__((always_inline)) {
+#pragma unroll
+        for (int t = 0; t < 4; ++t) {
+            const int64_t j = j0 + 64 * t + lane;
+            dst[t] = j < c1 ? dr[j] : INFINITY;
+        }
+    };
+    ldv(c0, v);
+    for (int64_t j0 = c0; j0 < c1; j0 += 256) {
+        ldv(j0 + 256, vn);
+        bool any = false;
+#pragma unroll
+        for (int t = 0; t < 4; ++t) {
+            const int64_t j = j0 + 64 * t + lane;
+            if (v[t] != v[t]) v[t] = INFINITY;
+            any = any || (j < c1 && pair_less(v[t], (uint32_t)(base + j), thr_d, thr_i));
+        }
+        if (__ballot(any) != 0ull) {
+#pragma unroll
+            for (int t = 0; t < 4; ++t) {
+                const int64_t j = j0 + 64 * t + lane;
+                top.offer(j < c1, v[t], (uint32_t)(base + j), k, lane, thr_d, thr_i);
+            }
+        }
+#pragma unroll
+        for (int t = 0; t < 4; ++t) v[t] = vn[t];
     }
     float* od = part_d + ((int64_t)(part0 + s) * rows + row) * k;
     uint32_t* oi = part_i + ((int64_t)(part0 + s) * rows + row) * k;
@@ -456,7 +481,10 @@ __global__ __launch_bounds__(256) void topk_seg_kernel(const float* __restrict__
     }
 }
 
-constexpr int kSegL = 4096;
+#ifndef MIVQ_SEGL
+#define MIVQ_SEGL 4096
+#endif
+constexpr int kSegL = MIVQ_SEGL;
 
 int64_t flat_tiled_cols(int64_t nq, int64_t n) {
     int64_t bc = ((int64_t)1 << 26) / std::max<int64_t>(nq, 1);  // <= 256 MiB of distances per chunk

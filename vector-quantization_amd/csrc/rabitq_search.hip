@@ -86,22 +86,45 @@ __global__ __launch_bounds__(256) void rabitq_qprep_kernel(const float* __restri
         atomicAdd(&red_sum, part);  // integer: order-free
     }
     __syncthreads();
-    if (tid == 0) {
-        // the oracle's sequential chains
+    if (tid < 64) {
+        // the oracle's sequential chains (one lane each: qc in lane 0, qn in lane 1), over the
+        // row staged in LDS a wave at a time: the global loads of a whole row are in flight at
+        // once instead of one round trip per element of a serial loop (round 6: 213 -> ~20 us
+        // per 1000 queries at d = 3072)
+        __shared__ float s_q[256], s_c[256];
         float qc = 0.0f, qn = 0.0f;
-        for (int j = 0; j < d; ++j) {
-            const float r = __fsub_rn(qrow[j], centroid ? centroid[j] : 0.0f);
-            qc = __builtin_fmaf(r, r, qc);
-            qn = __builtin_fmaf(qrow[j], qrow[j], qn);
+        for (int j0 = 0; j0 < d; j0 += 256) {
+            const int nj = min(256, d - j0);
+            for (int t = tid; t < nj; t += 64) {
+                s_q[t] = qrow[j0 + t];
+                s_c[t] = centroid ? centroid[j0 + t] : 0.0f;
+            }
+            __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): this wave's own LDS stores
+            __builtin_amdgcn_wave_barrier();
+            if (tid < 2) {
+                for (int t = 0; t < nj; ++t) {
+                    const float qv = s_q[t];
+                    if (tid == 0) {
+                        const float r = __fsub_rn(qv, s_c[t]);
+                        qc = __builtin_fmaf(r, r, qc);
+                    } else {
+                        qn = __builtin_fmaf(qv, qv, qn);
+                    }
+                }
+            }
+            __builtin_amdgcn_wave_barrier();
         }
+        qn = __shfl(qn, 1);
         float c1 = 0.0f, c2 = 0.0f, c34 = 0.0f;
         if (qb > 0) {
             c1 = __fmul_rn(__fmul_rn(2.0f, delta), isd);
             c2 = __fmul_rn(__fmul_rn(2.0f, vmin), isd);
             c34 = __fmul_rn(isd, __fadd_rn(__fmul_rn(delta, (float)red_sum), __fmul_rn((float)d, vmin)));
         }
-        float* f = qf + a * kQfStride;
-        f[0] = c1; f[1] = c2; f[2] = c34; f[3] = qc; f[4] = qn; f[5] = isd; f[6] = (float)off; f[7] = 0.0f;
+        if (tid == 0) {
+            float* f = qf + a * kQfStride;
+            f[0] = c1; f[1] = c2; f[2] = c34; f[3] = qc; f[4] = qn; f[5] = isd; f[6] = (float)off; f[7] = 0.0f;
+        }
     }
 }
 
@@ -246,6 +269,135 @@ __global__ __launch_bounds__(kEstWaves * 64) void rabitq_est_mfma_kernel(
     }
 }
 
+// d % 128 == 0 (round 6): the same integer dot, 32 * NQB queries per workgroup.  rabitq_est_mfma_kernel
+// spends ~20 VALU (the 16-bit sign expansion to int8) per v_mfma_i32_32x32x32_i8, because its LDS
+// holds one 32-query block at full d; here the query bytes go through LDS in chunks of kEstKC
+// dims (two stages, loaded a chunk ahead), and each expansion of a lane's 16 sign bits feeds NQB
+// MFMAs, one per 32-query sub-block, whose accumulators stay in registers across the chunks.
+// Wave w owns the 32-code tile w of the workgroup's 256 codes (lane (r, h): code r, k-half h, as
+// above); its code bits for a chunk (kEstKC / 32 dwords of the row) are loaded a chunk ahead too.
+// Integer sums: any order gives the oracle's dot; the epilogue is the estimator in fp32 order.
+constexpr int kEstKC = 512;                 // dims per LDS chunk
+constexpr int kEstQP = kEstKC + 16;         // LDS pitch of a query row: 33 x 16 B, conflict-free b128 reads
+template <int NQB>
+__global__ __launch_bounds__(kEstWaves * 64) void rabitq_est_mq_kernel(
+    const uint8_t* __restrict__ codes, int64_t m, int d, const int8_t* __restrict__ qq, const float* __restrict__ qf,
+    int64_t nq, int metric, float* __restrict__ buf, unsigned nqb) {
+    constexpr int QR = 32 * NQB;                      // query rows per workgroup
+    constexpr int STAGE = QR * kEstQP;                // bytes per LDS stage
+    constexpr int NST = QR * (kEstKC / 16) / (kEstWaves * 64);  // 16-B staging pieces per thread
+    static_assert(NST >= 1 && QR * (kEstKC / 16) % (kEstWaves * 64) == 0, "staging split");
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    const int tid = threadIdx.x, w = tid >> 6, l = tid & 63, r = l & 31, h = l >> 5;
+    const unsigned qblk = blockIdx.x % nqb, cchunk = blockIdx.x / nqb;
+    const int64_t q0 = (int64_t)qblk * QR;
+    const int nb = d >> 3, cs = nb + 8;
+    const int nch = d / kEstKC + (d % kEstKC ? 1 : 0);
+    const int64_t cb = ((int64_t)cchunk * kEstWaves + w) * 32;  // this wave's tile
+    const int nc = (int)max<int64_t>(0, min<int64_t>(32, m - cb));
+    // rows past the chunk read row 0 of the matrix (in range) and are never written
+    const uint8_t* crow = codes + (nc > 0 && r < nc ? cb + r : 0) * cs;
+    // staging piece i of this thread: query row e / 32, 16-B column e % 32 of the chunk
+    u32x4a4 qv[NST];
+    auto load_q = [&](int c) __attribute__((always_inline)) {
+        const int kc = min(kEstKC, d - c * kEstKC);
+#pragma unroll
+        for (int i = 0; i < NST; ++i) {
+            const int e = tid + i * kEstWaves * 64, row = e >> 5, col = e & 31;
+            u32x4a4 v = {0u, 0u, 0u, 0u};
+            if (q0 + row < nq && 16 * col < kc)
+                v = *reinterpret_cast<const u32x4a4*>(qq + (q0 + row) * d + (int64_t)c * kEstKC + 16 * col);
+            qv[i] = v;
+        }
+    };
+    auto store_q = [&](int c) __attribute__((always_inline)) {
+        unsigned char* st = smem + (c & 1) * STAGE;
+#pragma unroll
+        for (int i = 0; i < NST; ++i) {
+            const int e = tid + i * kEstWaves * 64, row = e >> 5, col = e & 31;
+            *reinterpret_cast<uint4*>(st + row * kEstQP + 16 * col) = make_uint4(qv[i][0], qv[i][1], qv[i][2], qv[i][3]);
+        }
+    };
+    constexpr int NG = kEstKC / 128;  // 16-B code-bit groups per chunk (4 k-steps each)
+    u32x4a4 cg[NG], cgn[NG];
+    auto load_c = [&](int c, u32x4a4 (&dst)[NG]) __attribute__((always_inline)) {
+        const int ng = min(kEstKC, d - c * kEstKC) / 128;
+#pragma unroll
+        for (int g = 0; g < NG; ++g)
+            if (g < ng) dst[g] = *reinterpret_cast<const u32x4a4*>(crow + (c * kEstKC) / 8 + 16 * g);
+    };
+    v16i acc[NQB];
+#pragma unroll
+    for (int j = 0; j < NQB; ++j) acc[j] = (v16i){};
+    int pc = 0;
+    const int sh = 16 * h;
+    load_q(0);
+    load_c(0, cg);
+    store_q(0);
+    __syncthreads();
+    for (int c = 0; c < nch; ++c) {
+        const bool more = c + 1 < nch;  // uniform
+        if (more) {
+            load_q(c + 1);
+            load_c(c + 1, cgn);
+        }
+        const int ng = min(kEstKC, d - c * kEstKC) / 128;
+        const int8_t* qs = reinterpret_cast<const int8_t*>(smem + (c & 1) * STAGE) + r * kEstQP + 16 * h;
+#pragma unroll
+        for (int g = 0; g < NG; ++g) {
+            if (g < ng) {
+#pragma unroll
+                for (int u = 0; u < 4; ++u) {
+                    const uint32_t b16 = (cg[g][u] >> sh) & 0xFFFFu;
+                    pc += __builtin_popcount(b16);
+                    v4i av;
+#pragma unroll
+                    for (int j = 0; j < 4; ++j) av[j] = (int)(__umul24((b16 >> (4 * j)) & 0xFu, 0x204081u) & 0x01010101u);
+                    const int s = 4 * g + u;  // k-step within the chunk
+#pragma unroll
+                    for (int jb = 0; jb < NQB; ++jb) {
+                        const v4i bq = *reinterpret_cast<const v4i*>(qs + jb * 32 * kEstQP + 32 * s);
+                        acc[jb] = __builtin_amdgcn_mfma_i32_32x32x32_i8(av, bq, acc[jb], 0, 0, 0);
+                    }
+                }
+            }
+        }
+        if (more) {
+            store_q(c + 1);
+#pragma unroll
+            for (int g = 0; g < NG; ++g) cg[g] = cgn[g];
+        }
+        __syncthreads();
+    }
+    if (nc <= 0) return;  // wave-uniform (after the last barrier)
+    const float fr = *reinterpret_cast<const float*>(crow + nb + 4 * h);  // h = 0: f0, h = 1: f1 of code r
+    const bool ip = metric == MIVQ_METRIC_INNER_PRODUCT;
+#pragma unroll
+    for (int jb = 0; jb < NQB; ++jb) {
+        const int64_t qa = q0 + 32 * jb + r;
+        const bool qok = qa < nq;
+        float c1 = 0.0f, c2 = 0.0f, c34 = 0.0f, qc = 0.0f, qn = 0.0f;
+        int off = 0;
+        if (qok) {
+            const float* f = qf + qa * kQfStride;
+            c1 = f[0]; c2 = f[1]; c34 = f[2]; qc = f[3]; qn = f[4]; off = (int)f[6];
+        }
+        float* orow = buf + (qok ? qa : 0) * m + cb;
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                const int ci = 8 * g + 4 * h + u;  // code row of accumulator 4g + u
+                const int pop = __shfl(pc, ci) + __shfl(pc, ci + 32);
+                const float f0 = __shfl(fr, ci), f1 = __shfl(fr, ci + 32);
+                const int dot = acc[jb][4 * g + u] + off * pop;
+                const float fd = __builtin_fmaf(c1, (float)dot, __builtin_fmaf(c2, (float)pop, -c34));
+                if (qok && ci < nc) orow[ci] = rabitq_key(fd, f0, f1, qc, qn, ip);
+            }
+        }
+    }
+}
+
 // Any d, any qb: thread = code, blockIdx.y = query.
 __global__ __launch_bounds__(256) void rabitq_est_generic_kernel(const uint8_t* __restrict__ codes, int64_t m, int d,
                                                                  const int8_t* __restrict__ qq,
@@ -334,10 +486,17 @@ extern "C" int mivq_rabitq_search(const uint8_t* codes, int64_t n, int32_t d, co
         return e == hipSuccess ? MIVQ_OK : set_error(MIVQ_ERR_HIP, "rabitq_search: %s", hipGetErrorString(e));
     }
     const bool mfma = qb > 0 && (d % 32) == 0 && (reinterpret_cast<uintptr_t>(codes) % 4) == 0;
-    const size_t smem = (size_t)32 * (d + 16);
+    // the multi-query kernel for d % 128 == 0 (32, 64 or 128 queries per workgroup by nq)
+#ifndef MIVQ_RQ_MQ
+#define MIVQ_RQ_MQ 1
+#endif
+    const int nqb_mq = nq > 64 ? 4 : nq > 32 ? 2 : 1;
+    const bool mq = MIVQ_RQ_MQ && mfma && (d % 128) == 0;
+    const size_t smem = mq ? (size_t)2 * 32 * nqb_mq * kEstQP : (size_t)32 * (d + 16);
     if (mfma && smem > 160 * 1024) return set_error(MIVQ_ERR_UNSUPPORTED, "rabitq_search: d=%d too large", d);
+    auto mq_kernel = nqb_mq == 4 ? rabitq_est_mq_kernel<4> : nqb_mq == 2 ? rabitq_est_mq_kernel<2> : rabitq_est_mq_kernel<1>;
     if (mfma) {
-        hipError_t e = hipFuncSetAttribute((const void*)rabitq_est_mfma_kernel,
+        hipError_t e = hipFuncSetAttribute(mq ? (const void*)mq_kernel : (const void*)rabitq_est_mfma_kernel,
                                            hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);
         if (e != hipSuccess) return set_error(MIVQ_ERR_HIP, "rabitq_search: %s", hipGetErrorString(e));
     }
@@ -345,7 +504,11 @@ extern "C" int mivq_rabitq_search(const uint8_t* codes, int64_t n, int32_t d, co
     const hipError_t e = launch_tiled_topk(
         nq, n, k, id_offset, p + L.tiled, dists, ids, st, [&](int64_t c0, int64_t m, float* buf) {
             const uint8_t* cc = codes + c0 * nbytes;
-            if (mfma)
+            if (mq) {
+                const unsigned nqblk = (unsigned)ceil_div(nq, 32 * nqb_mq);
+                hipLaunchKernelGGL(mq_kernel, dim3((unsigned)(ceil_div(m, kEstWaves * 32) * nqblk)),
+                                   dim3(kEstWaves * 64), smem, st, cc, m, d, qq, qf, nq, metric, buf, nqblk);
+            } else if (mfma)
                 hipLaunchKernelGGL(rabitq_est_mfma_kernel,
                                    dim3((unsigned)(ceil_div(m, kEstWaves * kEstTiles * 32) * ceil_div(nq, 32))),
                                    dim3(kEstWaves * 64), smem, st, cc, m, d, qq, qf, nq, metric, buf,

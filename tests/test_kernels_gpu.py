@@ -545,6 +545,8 @@ def test_kmeans_update_deterministic(dev, n, M, ksub, dsub):
     (5, 300, 64, 0, 8),         # qb = 0: float estimator (generic kernel)
     (3, 5, 64, 4, 10),          # fewer codes than k: sentinel slots
     (16500, 8500, 32, 4, 3),    # three column chunks of the tiled top-k
+    (150, 3000, 512, 4, 10),    # multi-query kernel, 128 queries per workgroup, ragged last block
+    (1000, 20000, 512, 4, 10),  # persistent multi-query kernel: each workgroup walks several code groups
 ])
 @pytest.mark.parametrize("metric", [1, 0])
 def test_rabitq_search_bit_exact(dev, oracle, nq, n, d, qb, k, metric):

@@ -481,10 +481,10 @@ __global__ __launch_bounds__(256) void topk_seg_kernel(const float* __restrict__
     }
 }
 
-#ifndef MIVQ_SEGL
-#define MIVQ_SEGL 4096
-#endif
-constexpr int kSegL = MIVQ_SEGL;
+// columns per segment (round 6: 16384 measured 3 % faster on the 1000 x 1M estimator search,
+// 1024 30 % slower, profiles/r06_s6; 4096 kept: flat_tiled_cols never goes below one segment,
+// so a longer segment would also raise the distance buffer's floor to nq x kSegL floats)
+constexpr int kSegL = 4096;
 
 int64_t flat_tiled_cols(int64_t nq, int64_t n) {
     int64_t bc = ((int64_t)1 << 26) / std::max<int64_t>(nq, 1);  // <= 256 MiB of distances per chunk

@@ -87,34 +87,38 @@ __global__ __launch_bounds__(256) void rabitq_qprep_kernel(const float* __restri
     }
     __syncthreads();
     if (tid < 64) {
-        // the oracle's sequential chains (one lane each: qc in lane 0, qn in lane 1), over the
-        // row staged in LDS a wave at a time: the global loads of a whole row are in flight at
-        // once instead of one round trip per element of a serial loop (round 6: 213 -> ~20 us
-        // per 1000 queries at d = 3072)
-        __shared__ float s_q[256], s_c[256];
+        // the oracle's sequential chains, both in lane 0, over the row staged in LDS 1024
+        // elements at a time by the whole wave: the global loads of a piece are in flight at
+        // once instead of one round trip per element of a serial loop
+        __shared__ __attribute__((aligned(16))) float s_q[1024], s_c[1024];
         float qc = 0.0f, qn = 0.0f;
-        for (int j0 = 0; j0 < d; j0 += 256) {
-            const int nj = min(256, d - j0);
+        for (int j0 = 0; j0 < d; j0 += 1024) {
+            const int nj = min(1024, d - j0);
             for (int t = tid; t < nj; t += 64) {
                 s_q[t] = qrow[j0 + t];
                 s_c[t] = centroid ? centroid[j0 + t] : 0.0f;
             }
             __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): this wave's own LDS stores
             __builtin_amdgcn_wave_barrier();
-            if (tid < 2) {
-                for (int t = 0; t < nj; ++t) {
-                    const float qv = s_q[t];
-                    if (tid == 0) {
-                        const float r = __fsub_rn(qv, s_c[t]);
-                        qc = __builtin_fmaf(r, r, qc);
-                    } else {
-                        qn = __builtin_fmaf(qv, qv, qn);
-                    }
+            if (tid == 0) {  // both chains in lane 0, 16-B LDS reads running ahead of the fmas
+                int t = 0;
+#pragma unroll 4
+                for (; t + 4 <= nj; t += 4) {
+                    const float4 qv = *reinterpret_cast<const float4*>(s_q + t);
+                    const float4 cv = *reinterpret_cast<const float4*>(s_c + t);
+                    float r = __fsub_rn(qv.x, cv.x); qc = __builtin_fmaf(r, r, qc); qn = __builtin_fmaf(qv.x, qv.x, qn);
+                    r = __fsub_rn(qv.y, cv.y); qc = __builtin_fmaf(r, r, qc); qn = __builtin_fmaf(qv.y, qv.y, qn);
+                    r = __fsub_rn(qv.z, cv.z); qc = __builtin_fmaf(r, r, qc); qn = __builtin_fmaf(qv.z, qv.z, qn);
+                    r = __fsub_rn(qv.w, cv.w); qc = __builtin_fmaf(r, r, qc); qn = __builtin_fmaf(qv.w, qv.w, qn);
+                }
+                for (; t < nj; ++t) {
+                    const float r = __fsub_rn(s_q[t], s_c[t]);
+                    qc = __builtin_fmaf(r, r, qc);
+                    qn = __builtin_fmaf(s_q[t], s_q[t], qn);
                 }
             }
             __builtin_amdgcn_wave_barrier();
         }
-        qn = __shfl(qn, 1);
         float c1 = 0.0f, c2 = 0.0f, c34 = 0.0f;
         if (qb > 0) {
             c1 = __fmul_rn(__fmul_rn(2.0f, delta), isd);
@@ -269,7 +273,7 @@ __global__ __launch_bounds__(kEstWaves * 64) void rabitq_est_mfma_kernel(
     }
 }
 
-// d % 128 == 0 (round 6): the same integer dot, 32 * NQB queries per workgroup.  rabitq_est_mfma_kernel
+// d % 512 == 0 (round 6): the same integer dot, 32 * NQB queries per workgroup.  rabitq_est_mfma_kernel
 // spends ~20 VALU (the 16-bit sign expansion to int8) per v_mfma_i32_32x32x32_i8, because its LDS
 // holds one 32-query block at full d; here the query bytes go through LDS in chunks of kEstKC
 // dims (two stages, loaded a chunk ahead), and each expansion of a lane's 16 sign bits feeds NQB
@@ -277,6 +281,13 @@ __global__ __launch_bounds__(kEstWaves * 64) void rabitq_est_mfma_kernel(
 // Wave w owns the 32-code tile w of the workgroup's 256 codes (lane (r, h): code r, k-half h, as
 // above); its code bits for a chunk (kEstKC / 32 dwords of the row) are loaded a chunk ahead too.
 // Integer sums: any order gives the oracle's dot; the epilogue is the estimator in fp32 order.
+// Workgroup barrier for LDS hand-offs only: waits for this wave's LDS (and scalar) operations,
+// not its global ones.  __syncthreads() is a workgroup release/acquire fence as well, so every
+// chunk's barrier would also wait for the loads prefetching the next chunk and for the
+// scattered key stores of the epilogue (vmcnt(0)).  The "memory" clobber keeps the compiler
+// from moving memory operations across it.
+__device__ __forceinline__ void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
+
 constexpr int kEstKC = 512;                 // dims per LDS chunk
 constexpr int kEstQP = kEstKC + 16;         // LDS pitch of a query row: 33 x 16 B, conflict-free b128 reads
 template <int NQB>
@@ -286,115 +297,164 @@ __global__ __launch_bounds__(kEstWaves * 64) void rabitq_est_mq_kernel(
     constexpr int QR = 32 * NQB;                      // query rows per workgroup
     constexpr int STAGE = QR * kEstQP;                // bytes per LDS stage
     constexpr int NST = QR * (kEstKC / 16) / (kEstWaves * 64);  // 16-B staging pieces per thread
-    static_assert(NST >= 1 && QR * (kEstKC / 16) % (kEstWaves * 64) == 0, "staging split");
+    static_assert(NST >= 2 && NST % 2 == 0 && QR * (kEstKC / 16) % (kEstWaves * 64) == 0, "staging split");
+    constexpr int NG = kEstKC / 128;  // 16-B code-bit groups per chunk (4 k-steps each)
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     const int tid = threadIdx.x, w = tid >> 6, l = tid & 63, r = l & 31, h = l >> 5;
-    const unsigned qblk = blockIdx.x % nqb, cchunk = blockIdx.x / nqb;
+    // persistent: workgroup b keeps query block b % nqb and walks the 256-code groups
+    // b / nqb, + gridDim.x / nqb, ... (gridDim.x is a multiple of nqb), so the nqb workgroups of
+    // a code group still run side by side (its code bits read from HBM once, then from L2)
+    const unsigned qblk = blockIdx.x % nqb;
+    const int64_t gstep = gridDim.x / nqb;
+    const int64_t ngroups = (m + kEstWaves * 32 - 1) / (kEstWaves * 32);
+    const int64_t g0 = blockIdx.x / nqb;
     const int64_t q0 = (int64_t)qblk * QR;
     const int nb = d >> 3, cs = nb + 8;
-    const int nch = d / kEstKC + (d % kEstKC ? 1 : 0);
-    const int64_t cb = ((int64_t)cchunk * kEstWaves + w) * 32;  // this wave's tile
-    const int nc = (int)max<int64_t>(0, min<int64_t>(32, m - cb));
-    // rows past the chunk read row 0 of the matrix (in range) and are never written
-    const uint8_t* crow = codes + (nc > 0 && r < nc ? cb + r : 0) * cs;
-    // staging piece i of this thread: query row e / 32, 16-B column e % 32 of the chunk
-    u32x4a4 qv[NST];
-    auto load_q = [&](int c) __attribute__((always_inline)) {
-        const int kc = min(kEstKC, d - c * kEstKC);
+    const int nch = d / kEstKC;  // d % kEstKC == 0 (host)
+    const int64_t nit = g0 < ngroups ? ((ngroups - 1 - g0) / gstep + 1) * nch : 0;  // (group, chunk) steps
+    // staging: piece i of this thread is query row e / 32, 16-B column e % 32 of the chunk; the
+    // next chunk is staged in two halves (loaded at the start / middle of a step, stored at its
+    // middle / end) so only half of it is held in registers at a time
+    u32x4a4 qv[NST / 2];
+    auto load_q = [&](int c, int half) __attribute__((always_inline)) {
+        // unconditional loads (so the compiler can count them: a conditional load makes every
+        // later wait a vmcnt(0)); rows past nq read row nq - 1, whose keys are never stored
 #pragma unroll
-        for (int i = 0; i < NST; ++i) {
-            const int e = tid + i * kEstWaves * 64, row = e >> 5, col = e & 31;
-            u32x4a4 v = {0u, 0u, 0u, 0u};
-            if (q0 + row < nq && 16 * col < kc)
-                v = *reinterpret_cast<const u32x4a4*>(qq + (q0 + row) * d + (int64_t)c * kEstKC + 16 * col);
-            qv[i] = v;
+        for (int i = 0; i < NST / 2; ++i) {
+            const int e = tid + (half * (NST / 2) + i) * kEstWaves * 64, row = e >> 5, col = e & 31;
+            const int64_t qr = min<int64_t>(q0 + row, nq - 1);
+            qv[i] = *reinterpret_cast<const u32x4a4*>(qq + qr * d + (int64_t)c * kEstKC + 16 * col);
         }
     };
-    auto store_q = [&](int c) __attribute__((always_inline)) {
-        unsigned char* st = smem + (c & 1) * STAGE;
+    auto store_q = [&](int st, int half) __attribute__((always_inline)) {
+        unsigned char* sp = smem + st * STAGE;
 #pragma unroll
-        for (int i = 0; i < NST; ++i) {
-            const int e = tid + i * kEstWaves * 64, row = e >> 5, col = e & 31;
-            *reinterpret_cast<uint4*>(st + row * kEstQP + 16 * col) = make_uint4(qv[i][0], qv[i][1], qv[i][2], qv[i][3]);
+        for (int i = 0; i < NST / 2; ++i) {
+            const int e = tid + (half * (NST / 2) + i) * kEstWaves * 64, row = e >> 5, col = e & 31;
+            *reinterpret_cast<uint4*>(sp + row * kEstQP + 16 * col) = make_uint4(qv[i][0], qv[i][1], qv[i][2], qv[i][3]);
         }
     };
-    constexpr int NG = kEstKC / 128;  // 16-B code-bit groups per chunk (4 k-steps each)
+    // this wave's code tile of group g; rows past m read row 0 (in range) and are never written
+    auto tile = [&](int64_t g, int& nc) -> const uint8_t* {
+        const int64_t cb = (g * kEstWaves + w) * 32;
+        nc = (int)max<int64_t>(0, min<int64_t>(32, m - cb));
+        return codes + (nc > 0 && r < nc ? cb + r : 0) * cs;
+    };
+    // the code bits of a chunk (NG 16-B groups of the row), loaded a whole step ahead
     u32x4a4 cg[NG], cgn[NG];
-    auto load_c = [&](int c, u32x4a4 (&dst)[NG]) __attribute__((always_inline)) {
-        const int ng = min(kEstKC, d - c * kEstKC) / 128;
+    auto load_c = [&](const uint8_t* crow, int c, u32x4a4 (&dst)[NG]) __attribute__((always_inline)) {
 #pragma unroll
-        for (int g = 0; g < NG; ++g)
-            if (g < ng) dst[g] = *reinterpret_cast<const u32x4a4*>(crow + (c * kEstKC) / 8 + 16 * g);
+        for (int g = 0; g < NG; ++g) dst[g] = *reinterpret_cast<const u32x4a4*>(crow + (c * kEstKC) / 8 + 16 * g);
     };
     v16i acc[NQB];
 #pragma unroll
     for (int j = 0; j < NQB; ++j) acc[j] = (v16i){};
     int pc = 0;
     const int sh = 16 * h;
-    load_q(0);
-    load_c(0, cg);
-    store_q(0);
-    __syncthreads();
-    for (int c = 0; c < nch; ++c) {
-        const bool more = c + 1 < nch;  // uniform
-        if (more) {
-            load_q(c + 1);
-            load_c(c + 1, cgn);
-        }
-        const int ng = min(kEstKC, d - c * kEstKC) / 128;
-        const int8_t* qs = reinterpret_cast<const int8_t*>(smem + (c & 1) * STAGE) + r * kEstQP + 16 * h;
+    const bool ip = metric == MIVQ_METRIC_INNER_PRODUCT;
+    int64_t g = g0;
+    int c = 0;
+    int nc;
+    const uint8_t* crow = tile(g, nc);
+    if (nit > 0) {
+        load_c(crow, 0, cg);
+        load_q(0, 0);
+        store_q(0, 0);
+        load_q(0, 1);
+        store_q(0, 1);
+    }
+    lds_barrier();
+    for (int64_t it = 0; it < nit; ++it) {
+        // the next step's chunk (the next group's first one at the end of a group)
+        const bool more = it + 1 < nit;  // uniform
+        const int cn = c + 1 < nch ? c + 1 : 0;
+        const int64_t gn = c + 1 < nch ? g : g + gstep;
+        int ncn = nc;
+        const uint8_t* crown = crow;
+        if (gn != g) crown = tile(gn, ncn);
+        // unconditional (the last step reloads rows it already has), so every wait is counted;
+        // the staging half first: its mid-step store then waits for it alone, not for the
+        // code bits issued after it
+        load_q(more ? cn : c, 0);
+        load_c(more ? crown : crow, more ? cn : c, cgn);
+        __builtin_amdgcn_sched_barrier(0);  // issue them here (the scheduler sinks loads to their use)
+        constexpr int ks = kEstKC / 32;  // k-steps per chunk (d % kEstKC == 0)
+        const int8_t* qs = reinterpret_cast<const int8_t*>(smem + (it & 1) * STAGE) + r * kEstQP + 16 * h;
+        // the B operands (query bytes) of k-step s + 1 are read from LDS while step s's MFMAs run
+        v4i bq[NQB];
 #pragma unroll
-        for (int g = 0; g < NG; ++g) {
-            if (g < ng) {
+        for (int jb = 0; jb < NQB; ++jb) bq[jb] = *reinterpret_cast<const v4i*>(qs + jb * 32 * kEstQP);
+#pragma unroll
+        for (int gg = 0; gg < NG; ++gg) {
+            {
+                if (gg == NG / 2) {  // mid-chunk: first staging half out, second in
+                    store_q((int)((it + 1) & 1), 0);  // unconditional: the last step's copy is never read
+                    load_q(more ? cn : c, 1);
+                    __builtin_amdgcn_sched_barrier(0);
+                }
 #pragma unroll
                 for (int u = 0; u < 4; ++u) {
-                    const uint32_t b16 = (cg[g][u] >> sh) & 0xFFFFu;
+                    const int s = 4 * gg + u;  // k-step within the chunk
+                    const int sn = s + 1 < ks ? s + 1 : s;
+                    v4i bqn[NQB];
+#pragma unroll
+                    for (int jb = 0; jb < NQB; ++jb) bqn[jb] = *reinterpret_cast<const v4i*>(qs + jb * 32 * kEstQP + 32 * sn);
+                    // keeps those reads here, ahead of this step's MFMAs (the scheduler would sink
+                    // them next to their use, exposing one LDS latency per MFMA)
+                    __builtin_amdgcn_sched_barrier(0);
+                    const uint32_t b16 = (cg[gg][u] >> sh) & 0xFFFFu;
                     pc += __builtin_popcount(b16);
                     v4i av;
 #pragma unroll
                     for (int j = 0; j < 4; ++j) av[j] = (int)(__umul24((b16 >> (4 * j)) & 0xFu, 0x204081u) & 0x01010101u);
-                    const int s = 4 * g + u;  // k-step within the chunk
 #pragma unroll
-                    for (int jb = 0; jb < NQB; ++jb) {
-                        const v4i bq = *reinterpret_cast<const v4i*>(qs + jb * 32 * kEstQP + 32 * s);
-                        acc[jb] = __builtin_amdgcn_mfma_i32_32x32x32_i8(av, bq, acc[jb], 0, 0, 0);
+                    for (int jb = 0; jb < NQB; ++jb) acc[jb] = __builtin_amdgcn_mfma_i32_32x32x32_i8(av, bq[jb], acc[jb], 0, 0, 0);
+#pragma unroll
+                    for (int jb = 0; jb < NQB; ++jb) bq[jb] = bqn[jb];
+                }
+            }
+        }
+        if (c + 1 == nch && nc > 0) {  // the group's last chunk: estimator epilogue (wave-uniform)
+            const int64_t cb = (g * kEstWaves + w) * 32;
+            const float fr = *reinterpret_cast<const float*>(crow + nb + 4 * h);  // h = 0: f0, 1: f1 of code r
+#pragma unroll
+            for (int jb = 0; jb < NQB; ++jb) {
+                const int64_t qa = q0 + 32 * jb + r;
+                const bool qok = qa < nq;
+                float c1 = 0.0f, c2 = 0.0f, c34 = 0.0f, qc = 0.0f, qn = 0.0f;
+                int off = 0;
+                if (qok) {
+                    const float* f = qf + qa * kQfStride;
+                    c1 = f[0]; c2 = f[1]; c34 = f[2]; qc = f[3]; qn = f[4]; off = (int)f[6];
+                }
+                float* orow = buf + (qok ? qa : 0) * m + cb;
+#pragma unroll
+                for (int g4 = 0; g4 < 4; ++g4) {
+#pragma unroll
+                    for (int u = 0; u < 4; ++u) {
+                        const int ci = 8 * g4 + 4 * h + u;  // code row of accumulator 4 g4 + u
+                        const int pop = __shfl(pc, ci) + __shfl(pc, ci + 32);
+                        const float f0 = __shfl(fr, ci), f1 = __shfl(fr, ci + 32);
+                        const int dot = acc[jb][4 * g4 + u] + off * pop;
+                        const float fd = __builtin_fmaf(c1, (float)dot, __builtin_fmaf(c2, (float)pop, -c34));
+                        if (qok && ci < nc) orow[ci] = rabitq_key(fd, f0, f1, qc, qn, ip);
                     }
                 }
             }
         }
-        if (more) {
-            store_q(c + 1);
+        if (c + 1 == nch) {
 #pragma unroll
-            for (int g = 0; g < NG; ++g) cg[g] = cgn[g];
+            for (int jb = 0; jb < NQB; ++jb) acc[jb] = (v16i){};
+            pc = 0;
         }
-        __syncthreads();
-    }
-    if (nc <= 0) return;  // wave-uniform (after the last barrier)
-    const float fr = *reinterpret_cast<const float*>(crow + nb + 4 * h);  // h = 0: f0, h = 1: f1 of code r
-    const bool ip = metric == MIVQ_METRIC_INNER_PRODUCT;
+        store_q((int)((it + 1) & 1), 1);
 #pragma unroll
-    for (int jb = 0; jb < NQB; ++jb) {
-        const int64_t qa = q0 + 32 * jb + r;
-        const bool qok = qa < nq;
-        float c1 = 0.0f, c2 = 0.0f, c34 = 0.0f, qc = 0.0f, qn = 0.0f;
-        int off = 0;
-        if (qok) {
-            const float* f = qf + qa * kQfStride;
-            c1 = f[0]; c2 = f[1]; c34 = f[2]; qc = f[3]; qn = f[4]; off = (int)f[6];
-        }
-        float* orow = buf + (qok ? qa : 0) * m + cb;
-#pragma unroll
-        for (int g = 0; g < 4; ++g) {
-#pragma unroll
-            for (int u = 0; u < 4; ++u) {
-                const int ci = 8 * g + 4 * h + u;  // code row of accumulator 4g + u
-                const int pop = __shfl(pc, ci) + __shfl(pc, ci + 32);
-                const float f0 = __shfl(fr, ci), f1 = __shfl(fr, ci + 32);
-                const int dot = acc[jb][4 * g + u] + off * pop;
-                const float fd = __builtin_fmaf(c1, (float)dot, __builtin_fmaf(c2, (float)pop, -c34));
-                if (qok && ci < nc) orow[ci] = rabitq_key(fd, f0, f1, qc, qn, ip);
-            }
-        }
+        for (int gg = 0; gg < NG; ++gg) cg[gg] = cgn[gg];
+        lds_barrier();
+        c = cn;
+        g = gn;
+        crow = crown;
+        nc = ncn;
     }
 }
 
@@ -486,12 +546,12 @@ extern "C" int mivq_rabitq_search(const uint8_t* codes, int64_t n, int32_t d, co
         return e == hipSuccess ? MIVQ_OK : set_error(MIVQ_ERR_HIP, "rabitq_search: %s", hipGetErrorString(e));
     }
     const bool mfma = qb > 0 && (d % 32) == 0 && (reinterpret_cast<uintptr_t>(codes) % 4) == 0;
-    // the multi-query kernel for d % 128 == 0 (32, 64 or 128 queries per workgroup by nq)
+    // the multi-query kernel for d % 512 == 0 (32, 64 or 128 queries per workgroup by nq)
 #ifndef MIVQ_RQ_MQ
 #define MIVQ_RQ_MQ 1
 #endif
     const int nqb_mq = nq > 64 ? 4 : nq > 32 ? 2 : 1;
-    const bool mq = MIVQ_RQ_MQ && mfma && (d % 128) == 0;
+    const bool mq = MIVQ_RQ_MQ && mfma && (d % kEstKC) == 0;
     const size_t smem = mq ? (size_t)2 * 32 * nqb_mq * kEstQP : (size_t)32 * (d + 16);
     if (mfma && smem > 160 * 1024) return set_error(MIVQ_ERR_UNSUPPORTED, "rabitq_search: d=%d too large", d);
     auto mq_kernel = nqb_mq == 4 ? rabitq_est_mq_kernel<4> : nqb_mq == 2 ? rabitq_est_mq_kernel<2> : rabitq_est_mq_kernel<1>;
@@ -505,9 +565,12 @@ extern "C" int mivq_rabitq_search(const uint8_t* codes, int64_t n, int32_t d, co
         nq, n, k, id_offset, p + L.tiled, dists, ids, st, [&](int64_t c0, int64_t m, float* buf) {
             const uint8_t* cc = codes + c0 * nbytes;
             if (mq) {
-                const unsigned nqblk = (unsigned)ceil_div(nq, 32 * nqb_mq);
-                hipLaunchKernelGGL(mq_kernel, dim3((unsigned)(ceil_div(m, kEstWaves * 32) * nqblk)),
-                                   dim3(kEstWaves * 64), smem, st, cc, m, d, qq, qf, nq, metric, buf, nqblk);
+                // persistent grid: a multiple of the query blocks, about one workgroup per CU
+                const int64_t nqblk = ceil_div(nq, 32 * nqb_mq);
+                const int64_t groups = ceil_div(m, kEstWaves * 32);
+                const int64_t per = std::max<int64_t>(1, std::min<int64_t>(groups, 256 / std::max<int64_t>(1, nqblk)));
+                hipLaunchKernelGGL(mq_kernel, dim3((unsigned)(per * nqblk)), dim3(kEstWaves * 64), smem, st, cc, m, d,
+                                   qq, qf, nq, metric, buf, (unsigned)nqblk);
             } else if (mfma)
                 hipLaunchKernelGGL(rabitq_est_mfma_kernel,
                                    dim3((unsigned)(ceil_div(m, kEstWaves * kEstTiles * 32) * ceil_div(nq, 32))),

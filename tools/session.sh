@@ -1,11 +1,17 @@
 #!/bin/bash
-# round 6 session 12: merged resolve split over two workgroups per list (this) vs one (split1)
+# Round-end evidence session (round 6): full GPU suite, smoke, PMC traffic passes
+# (profiles/traffic.json), kernel-trace splits by call size at 1M and 10M rows, ADC and RaBitQ
+# estimator splits and PMC, the VALU issue-rate probe (the ADC roofline's peak), the
+# streaming-sweep device rate, the default bench
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
-mkdir -p gpurun_out
-bash tools/gpu_session.sh \
-  "python -u -m pytest tests/test_kernels_gpu.py -k 'pq or slice' tests/test_pinning_gpu.py tests/test_opq_gpu.py -q -x --timeout 120 --timeout-method thread" \
-  "python tools/ab_lib.py vector-quantization_amd/lib/ab/libmivq_split1.so --reps 20" \
-  "python tools/ab_lib.py vector-quantization_amd/lib/ab/libmivq_split1.so --reps 10 --M 8" \
-  "python tools/ab_lib.py vector-quantization_amd/lib/ab/libmivq_split1.so --reps 10 --M 32" \
-  "python tools/ab_lib.py vector-quantization_amd/lib/ab/libmivq_split1.so --reps 6 --n 6650000 --d 1024" \
-  "python tools/ab_lib.py vector-quantization_amd/lib/ab/libmivq_split1.so --reps 4 --n 10000000"
+bash tools/gpu_session.sh pytest smoke \
+  "bash tools/pmc_traffic.sh" \
+  "bash tools/prof_split.sh r06_1m --steps 5 --warmup 2" \
+  "bash tools/prof_split.sh r06_10m --n 10000000 --no-adc --steps 3 --warmup 1" \
+  "timeout -k 5 60 ./tools/probes/valu_rate" \
+  "bash tools/adc_split.sh 1m" \
+  "bash tools/adc_split.sh c5 --n 6650000 --d 1024 --nq 10000" \
+  "bash tools/pmc_qscan.sh fin_1m" \
+  "bash tools/pmc_qscan.sh fin_c5 --n 6650000 --d 1024 --nq 10000" \
+  "python -u tools/stream_rate.py" \
+  "python -u bench.py"

@@ -567,6 +567,43 @@ def test_rabitq_search_bit_exact(dev, oracle, nq, n, d, qb, k, metric):
     np.testing.assert_array_equal(_h(kd), rd)
 
 
+@pytest.mark.parametrize("k,metric,order", [
+    (10, 1, "worst"),     # every later code beats every earlier one for query 0: all pass the screen
+    (100, 1, "random"),   # two-register lists
+    (256, 0, "worst"),    # k = 256, inner product
+    (10, 0, "random"),
+])
+def test_rabitq_search_screened_blocks(dev, oracle, k, metric, order):
+    """The screened search of the multi-query kernel (d % 512 == 0): a dense first block (two
+    column chunks of the tiled top-k at nq = 4100), then screened blocks whose keys are appended
+    only when they beat the query's running k-th element, merged in place.  Codes ordered so
+    that query 0 finds a better code at every later position (its lists hold whole blocks),
+    exact duplicates of first-block codes in later blocks (ties must keep the smaller id), a
+    ragged last query block; checked against the oracle on a subset of the queries."""
+    from haag_vq import _native
+
+    rng = np.random.default_rng(k + metric)
+    nq, n, d = 4100, 40000, 512
+    X = rng.standard_normal((n, d)).astype(np.float32)
+    Q = rng.standard_normal((nq, d)).astype(np.float32)
+    c = X.mean(0).astype(np.float32)
+    cd = _t(c, dev)
+    codes = _h(_native.rabitq_encode(_t(X, dev), cd, metric))
+    if order == "worst":
+        keys0 = oracle.rabitq_est(codes, d, Q[:1], c, 4, metric)[0]
+        codes = codes[np.argsort(-keys0, kind="stable")]
+    dup_src = rng.choice(8000, 300, replace=False)
+    dup_dst = 16384 + rng.choice(n - 16384, 300, replace=False)
+    codes[dup_dst] = codes[dup_src]
+    codes = np.ascontiguousarray(codes)
+    kd, ki = _native.rabitq_search(_t(codes, dev), d, cd, _t(Q, dev), 4, metric, k)
+    sub = np.r_[0, 1, 31, 32, 127, 128, 2049, rng.choice(nq, 24, replace=False), nq - 4, nq - 1]
+    keys = oracle.rabitq_est(codes, d, Q[sub], c, 4, metric)
+    rd, ri = oracle.topk_rows(keys, k)
+    np.testing.assert_array_equal(_h(ki)[sub].view(np.uint32), ri)
+    np.testing.assert_array_equal(_h(kd)[sub], rd)
+
+
 @pytest.mark.parametrize("d", [96, 192])
 def test_pq_encode_slice_boundary_wide_shapes(dev, oracle, d):
     """the slicing of large calls (2^20-row slices since round 5) at the shapes it was

@@ -502,6 +502,8 @@ hipError_t launch_topk_seg(const float* dist, int64_t rows, int64_t ld, int64_t 
 
 }  // namespace
 
+int64_t tiled_topk_cols(int64_t nq, int64_t n) { return flat_tiled_cols(nq, n); }
+
 size_t flat_tiled_workspace_bytes(int64_t nq, int64_t n, int k) {
     const int64_t bc = flat_tiled_cols(nq, n);
     const int64_t S = bc / kSegL;

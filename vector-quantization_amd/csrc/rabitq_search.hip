@@ -290,10 +290,28 @@ __device__ __forceinline__ void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(
 
 constexpr int kEstKC = 512;                 // dims per LDS chunk
 constexpr int kEstQP = kEstKC + 16;         // LDS pitch of a query row: 33 x 16 B, conflict-free b128 reads
-template <int NQB>
+
+// Screened key blocks (round 6, the multi-query kernel after the first column block): instead of
+// the dense (nq, m) key block, a key is kept only when it ranks before the query's current k-th
+// element (run_d / run_i: the running (nq, k) top-k of the blocks before, element k - 1), and is
+// appended with its id to the query's candidate list (cnt[q] entries of row q, pitch ldc >= m, so
+// no list can overflow).  Every key that can enter the final top-k passes the screen, so merging
+// the lists into the running top-k gives the same (key, id) list as the dense block's top-k.
+struct RqScreen {
+    const float* run_d;
+    const uint32_t* run_i;
+    int k;
+    uint32_t* cnt;
+    float* cand_d;
+    uint32_t* cand_i;
+    int64_t ldc;
+    uint32_t idbase;  // id of the block's column 0 (id_offset + c0, uint32 as in the dense path)
+};
+
+template <int NQB, bool SCREEN>
 __global__ __launch_bounds__(kEstWaves * 64) void rabitq_est_mq_kernel(
     const uint8_t* __restrict__ codes, int64_t m, int d, const int8_t* __restrict__ qq, const float* __restrict__ qf,
-    int64_t nq, int metric, float* __restrict__ buf, unsigned nqb) {
+    int64_t nq, int metric, float* __restrict__ buf, unsigned nqb, RqScreen scr) {
     constexpr int QR = 32 * NQB;                      // query rows per workgroup
     constexpr int STAGE = QR * kEstQP;                // bytes per LDS stage
     constexpr int NST = QR * (kEstKC / 16) / (kEstWaves * 64);  // 16-B staging pieces per thread
@@ -423,9 +441,16 @@ __global__ __launch_bounds__(kEstWaves * 64) void rabitq_est_mq_kernel(
                 const bool qok = qa < nq;
                 float c1 = 0.0f, c2 = 0.0f, c34 = 0.0f, qc = 0.0f, qn = 0.0f;
                 int off = 0;
+                // the screen's threshold: the query's k-th element (fixed for the launch)
+                float thd = INFINITY;
+                uint32_t thi = kNoId;
                 if (qok) {
                     const float* f = qf + qa * kQfStride;
                     c1 = f[0]; c2 = f[1]; c34 = f[2]; qc = f[3]; qn = f[4]; off = (int)f[6];
+                    if constexpr (SCREEN) {
+                        thd = scr.run_d[qa * scr.k + scr.k - 1];
+                        thi = scr.run_i[qa * scr.k + scr.k - 1];
+                    }
                 }
                 float* orow = buf + (qok ? qa : 0) * m + cb;
 #pragma unroll
@@ -437,7 +462,18 @@ __global__ __launch_bounds__(kEstWaves * 64) void rabitq_est_mq_kernel(
                         const float f0 = __shfl(fr, ci), f1 = __shfl(fr, ci + 32);
                         const int dot = acc[jb][4 * g4 + u] + off * pop;
                         const float fd = __builtin_fmaf(c1, (float)dot, __builtin_fmaf(c2, (float)pop, -c34));
-                        if (qok && ci < nc) orow[ci] = rabitq_key(fd, f0, f1, qc, qn, ip);
+                        if constexpr (SCREEN) {
+                            float key = rabitq_key(fd, f0, f1, qc, qn, ip);
+                            if (key != key) key = INFINITY;  // as the dense path's top-k
+                            const uint32_t id = scr.idbase + (uint32_t)(cb + ci);
+                            if (qok && ci < nc && pair_less(key, id, thd, thi)) {
+                                const int64_t slot = atomicAdd(scr.cnt + qa, 1u);
+                                scr.cand_d[qa * scr.ldc + slot] = key;
+                                scr.cand_i[qa * scr.ldc + slot] = id;
+                            }
+                        } else if (qok && ci < nc) {
+                            orow[ci] = rabitq_key(fd, f0, f1, qc, qn, ip);
+                        }
                     }
                 }
             }
@@ -456,6 +492,46 @@ __global__ __launch_bounds__(kEstWaves * 64) void rabitq_est_mq_kernel(
         crow = crown;
         nc = ncn;
     }
+}
+
+// Merges each query's screened candidates (RqScreen) into its running top-k in place, one wave
+// per query, and clears the query's count for the next block.  Exact in (key, id) whatever the
+// order the candidates were appended in.
+template <int R>
+__global__ __launch_bounds__(256) void rq_screen_merge_kernel(float* __restrict__ run_d, uint32_t* __restrict__ run_i,
+                                                              int64_t nq, int k, uint32_t* __restrict__ cnt,
+                                                              const float* __restrict__ cand_d,
+                                                              const uint32_t* __restrict__ cand_i, int64_t ldc) {
+    const int lane = threadIdx.x & 63;
+    const int64_t q = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (q >= nq) return;
+    const uint32_t nc = cnt[q];  // wave-uniform
+    if (nc == 0) return;
+    WaveTopK<R> top;
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+        const int e = r * 64 + lane;
+        top.d[r] = e < k ? run_d[q * k + e] : INFINITY;
+        top.id[r] = e < k ? run_i[q * k + e] : kNoId;
+    }
+    float thr_d;
+    uint32_t thr_i;
+    top.kth(k, thr_d, thr_i);
+    const float* cd = cand_d + q * ldc;
+    const uint32_t* cix = cand_i + q * ldc;
+    for (uint32_t j0 = 0; j0 < nc; j0 += 64) {
+        const uint32_t j = j0 + lane;
+        const bool valid = j < nc;
+        const float dv = valid ? cd[j] : INFINITY;
+        const uint32_t iv = valid ? cix[j] : kNoId;
+        top.offer(valid, dv, iv, k, lane, thr_d, thr_i);
+    }
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+        const int e = r * 64 + lane;
+        if (e < k) { run_d[q * k + e] = top.d[r]; run_i[q * k + e] = top.id[r]; }
+    }
+    if (lane == 0) cnt[q] = 0;
 }
 
 // Any d, any qb: thread = code, blockIdx.y = query.
@@ -493,19 +569,28 @@ __global__ __launch_bounds__(256) void rabitq_est_generic_kernel(const uint8_t* 
 }
 
 struct RqLayout {
-    size_t qq, qr, qf, tiled, total;
+    size_t qq, qr, qf, tiled, cand_i, cnt, total;
 };
 
+// The screened blocks' candidate keys reuse the tiled top-k's key block (nq x cols floats at the
+// start of its region); their ids and the per-query counts follow it.
 RqLayout rq_layout(int64_t nq, int64_t n, int d, int k) {
     RqLayout L{};
     size_t off = 0;
+    const bool screened = d % kEstKC == 0;
     L.qq = off;    off = align_up(off + (size_t)nq * d, 256);
     L.qr = off;    off = align_up(off + (size_t)nq * d * 4, 256);
     L.qf = off;    off = align_up(off + (size_t)nq * kQfStride * 4, 256);
     L.tiled = off; off = align_up(off + flat_tiled_workspace_bytes(nq, n, k), 256);
+    L.cand_i = off; off = align_up(off + (screened ? (size_t)nq * tiled_topk_cols(nq, n) * 4 : 0), 256);
+    L.cnt = off;   off = align_up(off + (screened ? (size_t)nq * 4 : 0), 256);
     L.total = off;
     return L;
 }
+
+// Columns of the dense first block of the screened search: its top-k gives every query a
+// threshold (the k-th best of 16384 keys passes ~k / 16384 of the keys after it).
+constexpr int64_t kRqFirstCols = 16384;
 
 }  // namespace
 }  // namespace mivq
@@ -554,24 +639,40 @@ extern "C" int mivq_rabitq_search(const uint8_t* codes, int64_t n, int32_t d, co
     const bool mq = MIVQ_RQ_MQ && mfma && (d % kEstKC) == 0;
     const size_t smem = mq ? (size_t)2 * 32 * nqb_mq * kEstQP : (size_t)32 * (d + 16);
     if (mfma && smem > 160 * 1024) return set_error(MIVQ_ERR_UNSUPPORTED, "rabitq_search: d=%d too large", d);
-    auto mq_kernel = nqb_mq == 4 ? rabitq_est_mq_kernel<4> : nqb_mq == 2 ? rabitq_est_mq_kernel<2> : rabitq_est_mq_kernel<1>;
+    using MqFn = void (*)(const uint8_t*, int64_t, int, const int8_t*, const float*, int64_t, int, float*, unsigned,
+                          RqScreen);
+    const MqFn mq_dense = nqb_mq == 4   ? rabitq_est_mq_kernel<4, false>
+                          : nqb_mq == 2 ? rabitq_est_mq_kernel<2, false>
+                                        : rabitq_est_mq_kernel<1, false>;
+    const MqFn mq_screen = nqb_mq == 4   ? rabitq_est_mq_kernel<4, true>
+                           : nqb_mq == 2 ? rabitq_est_mq_kernel<2, true>
+                                         : rabitq_est_mq_kernel<1, true>;
     if (mfma) {
-        hipError_t e = hipFuncSetAttribute(mq ? (const void*)mq_kernel : (const void*)rabitq_est_mfma_kernel,
-                                           hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);
-        if (e != hipSuccess) return set_error(MIVQ_ERR_HIP, "rabitq_search: %s", hipGetErrorString(e));
+        for (const void* f : {mq ? (const void*)mq_dense : (const void*)rabitq_est_mfma_kernel, (const void*)mq_screen}) {
+            hipError_t e = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);
+            if (e != hipSuccess) return set_error(MIVQ_ERR_HIP, "rabitq_search: %s", hipGetErrorString(e));
+        }
     }
     const int nbytes = (d + 7) / 8 + 8;
-    const hipError_t e = launch_tiled_topk(
-        nq, n, k, id_offset, p + L.tiled, dists, ids, st, [&](int64_t c0, int64_t m, float* buf) {
+    // persistent grid of the multi-query kernel: a multiple of the query blocks, about one
+    // workgroup per CU
+    auto launch_mq = [&](MqFn fn, int64_t c0, int64_t m, float* buf, const RqScreen& scr) {
+        const int64_t nqblk = ceil_div(nq, 32 * nqb_mq);
+        const int64_t groups = ceil_div(m, kEstWaves * 32);
+        const int64_t per = std::max<int64_t>(1, std::min<int64_t>(groups, 256 / std::max<int64_t>(1, nqblk)));
+        hipLaunchKernelGGL(fn, dim3((unsigned)(per * nqblk)), dim3(kEstWaves * 64), smem, st, codes + c0 * nbytes, m,
+                           d, qq, qf, nq, metric, buf, (unsigned)nqblk, scr);
+        return hipGetLastError();
+    };
+    // the dense key blocks and their tiled top-k: the whole search, or the first block of the
+    // screened one
+    const int64_t n_dense = mq ? std::min<int64_t>(n, kRqFirstCols) : n;
+    hipError_t e = launch_tiled_topk(
+        nq, n_dense, k, id_offset, p + L.tiled, dists, ids, st, [&](int64_t c0, int64_t m, float* buf) {
             const uint8_t* cc = codes + c0 * nbytes;
-            if (mq) {
-                // persistent grid: a multiple of the query blocks, about one workgroup per CU
-                const int64_t nqblk = ceil_div(nq, 32 * nqb_mq);
-                const int64_t groups = ceil_div(m, kEstWaves * 32);
-                const int64_t per = std::max<int64_t>(1, std::min<int64_t>(groups, 256 / std::max<int64_t>(1, nqblk)));
-                hipLaunchKernelGGL(mq_kernel, dim3((unsigned)(per * nqblk)), dim3(kEstWaves * 64), smem, st, cc, m, d,
-                                   qq, qf, nq, metric, buf, (unsigned)nqblk);
-            } else if (mfma)
+            if (mq)
+                return launch_mq(mq_dense, c0, m, buf, RqScreen{});
+            if (mfma)
                 hipLaunchKernelGGL(rabitq_est_mfma_kernel,
                                    dim3((unsigned)(ceil_div(m, kEstWaves * kEstTiles * 32) * ceil_div(nq, 32))),
                                    dim3(kEstWaves * 64), smem, st, cc, m, d, qq, qf, nq, metric, buf,
@@ -581,6 +682,32 @@ extern "C" int mivq_rabitq_search(const uint8_t* codes, int64_t n, int32_t d, co
                                    dim3(256), 0, st, cc, m, d, qq, qr, qf, qb, metric, buf);
             return hipGetLastError();
         });
+    if (e == hipSuccess && n > n_dense) {
+        // screened blocks of about equal size (at most the key block's columns, whole 256-code
+        // groups), each followed by the merge of its candidates into (dists, ids)
+        const int64_t cap = tiled_topk_cols(nq, n);
+        const int64_t rest = n - n_dense;
+        const int64_t nblk = ceil_div(rest, cap);
+        const int64_t cols = std::min<int64_t>(cap, ceil_div(ceil_div(rest, nblk), kEstWaves * 32) * (kEstWaves * 32));
+        uint32_t* cnt = reinterpret_cast<uint32_t*>(p + L.cnt);
+        RqScreen scr{dists, ids, k, cnt, reinterpret_cast<float*>(p + L.tiled),
+                     reinterpret_cast<uint32_t*>(p + L.cand_i), cap, 0u};
+        e = hipMemsetAsync(cnt, 0, (size_t)nq * 4, st);
+        for (int64_t c0 = n_dense; c0 < n && e == hipSuccess; c0 += cols) {
+            const int64_t m = std::min<int64_t>(cols, n - c0);
+            scr.idbase = (uint32_t)(id_offset + c0);
+            e = launch_mq(mq_screen, c0, m, nullptr, scr);
+            if (e != hipSuccess) break;
+            const dim3 grid((unsigned)ceil_div(nq, 4)), block(256);
+            switch ((k + 63) / 64) {
+                case 1: hipLaunchKernelGGL(rq_screen_merge_kernel<1>, grid, block, 0, st, dists, ids, nq, k, cnt, scr.cand_d, scr.cand_i, cap); break;
+                case 2: hipLaunchKernelGGL(rq_screen_merge_kernel<2>, grid, block, 0, st, dists, ids, nq, k, cnt, scr.cand_d, scr.cand_i, cap); break;
+                case 3: hipLaunchKernelGGL(rq_screen_merge_kernel<3>, grid, block, 0, st, dists, ids, nq, k, cnt, scr.cand_d, scr.cand_i, cap); break;
+                default: hipLaunchKernelGGL(rq_screen_merge_kernel<4>, grid, block, 0, st, dists, ids, nq, k, cnt, scr.cand_d, scr.cand_i, cap); break;
+            }
+            e = hipGetLastError();
+        }
+    }
     if (e != hipSuccess) return set_error(MIVQ_ERR_HIP, "rabitq_search: %s", hipGetErrorString(e));
     return MIVQ_OK;
 }

@@ -89,6 +89,9 @@ hipError_t launch_topk_merge(const float* pd, const uint32_t* pi, int parts, int
 using TileFn = std::function<hipError_t(int64_t c0, int64_t m, float* buf)>;
 hipError_t launch_tiled_topk(int64_t nq, int64_t n, int k, int64_t id_offset, void* ws, float* dists,
                              uint32_t* ids, hipStream_t st, const TileFn& tile);
+// Columns per key block of launch_tiled_topk (a multiple of its 4096-column segment; the key
+// block is nq x that many floats at the start of its workspace).
+int64_t tiled_topk_cols(int64_t nq, int64_t n);
 // Tiled exact brute force (ivf.hip): pairwise chains + segmented top-k + running merge.
 size_t flat_tiled_workspace_bytes(int64_t nq, int64_t n, int k);
 hipError_t launch_flat_tiled(const float* q, int64_t nq, const float* x, int64_t n, int d, int metric, int k,

@@ -23,6 +23,8 @@
 
 #include <math.h>
 
+#include <type_traits>
+
 namespace mivq {
 namespace {
 
@@ -322,10 +324,19 @@ __global__ __launch_bounds__(kEstWaves * 64) void rabitq_est_mq_kernel(
     // persistent: workgroup b keeps query block b % nqb and walks the 256-code groups
     // b / nqb, + gridDim.x / nqb, ... (gridDim.x is a multiple of nqb), so the nqb workgroups of
     // a code group still run side by side (its code bits read from HBM once, then from L2)
-    const unsigned qblk = blockIdx.x % nqb;
+#ifndef MIVQ_RQ_XCD
+#define MIVQ_RQ_XCD 0
+#endif
+    unsigned qblk = blockIdx.x % nqb;
     const int64_t gstep = gridDim.x / nqb;
     const int64_t ngroups = (m + kEstWaves * 32 - 1) / (kEstWaves * 32);
-    const int64_t g0 = blockIdx.x / nqb;
+    int64_t g0 = blockIdx.x / nqb;
+    if (MIVQ_RQ_XCD && gridDim.x % (8 * nqb) == 0) {
+        // the nqb workgroups of a code group on one XCD (blocks b and b + 8 share one)
+        const unsigned x = blockIdx.x % 8, j = blockIdx.x / 8;
+        qblk = j % nqb;
+        g0 = x + 8 * (j / nqb);
+    }
     const int64_t q0 = (int64_t)qblk * QR;
     const int nb = d >> 3, cs = nb + 8;
     const int nch = d / kEstKC;  // d % kEstKC == 0 (host)
@@ -334,14 +345,19 @@ __global__ __launch_bounds__(kEstWaves * 64) void rabitq_est_mq_kernel(
     // next chunk is staged in two halves (loaded at the start / middle of a step, stored at its
     // middle / end) so only half of it is held in registers at a time
     u32x4a4 qv[NST / 2];
+    // range-checked buffer loads over this block's query rows: rows past nq read zeros (their keys
+    // are never stored), the per-thread offset is one register and the piece / chunk offsets are
+    // scalar (unconditional loads: a conditional load makes every later wait a vmcnt(0))
+    const __amdgpu_buffer_rsrc_t qrs = __builtin_amdgcn_make_buffer_rsrc(
+        (void*)(qq + q0 * d), 0, (int)(max<int64_t>(0, min<int64_t>(QR, nq - q0)) * d), 0x00020000);
+    const int qvo = (tid >> 5) * d + 16 * (tid & 31);  // piece i: row (tid >> 5) + 16 i, column tid % 32
+    static_assert((kEstWaves * 64) % 32 == 0, "staging pieces keep the thread's column");
     auto load_q = [&](int c, int half) __attribute__((always_inline)) {
-        // unconditional loads (so the compiler can count them: a conditional load makes every
-        // later wait a vmcnt(0)); rows past nq read row nq - 1, whose keys are never stored
 #pragma unroll
         for (int i = 0; i < NST / 2; ++i) {
-            const int e = tid + (half * (NST / 2) + i) * kEstWaves * 64, row = e >> 5, col = e & 31;
-            const int64_t qr = min<int64_t>(q0 + row, nq - 1);
-            qv[i] = *reinterpret_cast<const u32x4a4*>(qq + qr * d + (int64_t)c * kEstKC + 16 * col);
+            const int pi = half * (NST / 2) + i;
+            const auto v = __builtin_amdgcn_raw_buffer_load_b128(qrs, qvo, pi * (kEstWaves * 64 / 32) * d + c * kEstKC, 0);
+            qv[i] = (u32x4a4){v[0], v[1], v[2], v[3]};
         }
     };
     auto store_q = [&](int st, int half) __attribute__((always_inline)) {
@@ -370,6 +386,22 @@ __global__ __launch_bounds__(kEstWaves * 64) void rabitq_est_mq_kernel(
     int pc = 0;
     const int sh = 16 * h;
     const bool ip = metric == MIVQ_METRIC_INNER_PRODUCT;
+    // per-query epilogue terms {c1, c2, c34, qc, qn, thd, off, thi} (thd / thi: the screen's
+    // threshold, fixed for the launch) and per-wave code terms {pc of k-half 0, 1; f0; f1}, read
+    // by the epilogue with b128 LDS reads instead of global loads and a shuffle per term
+    float* qinfo = reinterpret_cast<float*>(smem + 2 * STAGE);
+    float* cinfo = reinterpret_cast<float*>(smem + 2 * STAGE + QR * 32) + w * 128;
+    if (tid < QR) {
+        const int64_t qa = min<int64_t>(q0 + tid, nq - 1);
+        float4 fa = *reinterpret_cast<const float4*>(qf + qa * kQfStride);
+        float4 fb = *reinterpret_cast<const float4*>(qf + qa * kQfStride + 4);
+        if constexpr (SCREEN) {
+            fb.y = scr.run_d[qa * scr.k + scr.k - 1];
+            fb.w = __uint_as_float(scr.run_i[qa * scr.k + scr.k - 1]);
+        }
+        *reinterpret_cast<float4*>(qinfo + tid * 8) = fa;
+        *reinterpret_cast<float4*>(qinfo + tid * 8 + 4) = fb;
+    }
     int64_t g = g0;
     int c = 0;
     int nc;
@@ -382,6 +414,10 @@ __global__ __launch_bounds__(kEstWaves * 64) void rabitq_est_mq_kernel(
         store_q(0, 1);
     }
     lds_barrier();
+#ifndef MIVQ_RQ_PRIO
+#define MIVQ_RQ_PRIO 0
+#endif
+    if (MIVQ_RQ_PRIO && w >= kEstWaves / 2) __builtin_amdgcn_s_setprio(1);
     for (int64_t it = 0; it < nit; ++it) {
         // the next step's chunk (the next group's first one at the end of a group)
         const bool more = it + 1 < nit;  // uniform
@@ -435,48 +471,77 @@ __global__ __launch_bounds__(kEstWaves * 64) void rabitq_est_mq_kernel(
         if (c + 1 == nch && nc > 0) {  // the group's last chunk: estimator epilogue (wave-uniform)
             const int64_t cb = (g * kEstWaves + w) * 32;
             const float fr = *reinterpret_cast<const float*>(crow + nb + 4 * h);  // h = 0: f0, 1: f1 of code r
+            // per code r of the tile: pop (both k-halves), (float)pop, f0 and -2 f1 (exact), so that
+            // each (query, code) term below is 7 VALU: dot, 2 fma, convert, add, fma, compare
+            cinfo[32 * h + r] = __int_as_float(pc);
+            lds_fence();
+            const int pop_r = __float_as_int(cinfo[r]) + __float_as_int(cinfo[32 + r]);
+            if (h == 0) {
+                cinfo[r] = __int_as_float(pop_r);
+                cinfo[32 + r] = (float)pop_r;
+                cinfo[64 + r] = fr;
+            } else {
+                cinfo[96 + r] = __fmul_rn(-2.0f, fr);
+            }
+            lds_fence();  // this wave's own LDS stores, read back below by other lanes
+            auto epilogue = [&](auto ipc) __attribute__((always_inline)) {
+                constexpr bool IP = decltype(ipc)::value;
 #pragma unroll
-            for (int jb = 0; jb < NQB; ++jb) {
-                const int64_t qa = q0 + 32 * jb + r;
-                const bool qok = qa < nq;
-                float c1 = 0.0f, c2 = 0.0f, c34 = 0.0f, qc = 0.0f, qn = 0.0f;
-                int off = 0;
-                // the screen's threshold: the query's k-th element (fixed for the launch)
-                float thd = INFINITY;
-                uint32_t thi = kNoId;
-                if (qok) {
-                    const float* f = qf + qa * kQfStride;
-                    c1 = f[0]; c2 = f[1]; c34 = f[2]; qc = f[3]; qn = f[4]; off = (int)f[6];
-                    if constexpr (SCREEN) {
-                        thd = scr.run_d[qa * scr.k + scr.k - 1];
-                        thi = scr.run_i[qa * scr.k + scr.k - 1];
-                    }
-                }
-                float* orow = buf + (qok ? qa : 0) * m + cb;
+                for (int jb = 0; jb < NQB; ++jb) {
+                    const int64_t qa = q0 + 32 * jb + r;
+                    const bool qok = qa < nq;
+                    const float4 fa = *reinterpret_cast<const float4*>(qinfo + (32 * jb + r) * 8);
+                    const float4 fb = *reinterpret_cast<const float4*>(qinfo + (32 * jb + r) * 8 + 4);
+                    const float c1 = fa.x, c2 = fa.y, nc34 = -fa.z, qc = fa.w, qn = fb.x, thd = fb.y;
+                    const int off = (int)fb.z;
+                    float* orow = buf + (qok ? qa : 0) * m + cb;
 #pragma unroll
-                for (int g4 = 0; g4 < 4; ++g4) {
+                    for (int g4 = 0; g4 < 4; ++g4) {
+                        const int base = 8 * g4 + 4 * h;  // code rows of accumulators 4 g4 .. 4 g4 + 3
+                        const int4 pv = *reinterpret_cast<const int4*>(cinfo + base);
+                        const float4 pf = *reinterpret_cast<const float4*>(cinfo + 32 + base);
+                        const float4 f0v = *reinterpret_cast<const float4*>(cinfo + 64 + base);
+                        const float4 mf1 = *reinterpret_cast<const float4*>(cinfo + 96 + base);
+                        const int pa[4] = {pv.x, pv.y, pv.z, pv.w};
+                        const float pfa[4] = {pf.x, pf.y, pf.z, pf.w}, f0a[4] = {f0v.x, f0v.y, f0v.z, f0v.w},
+                                    m2f1[4] = {mf1.x, mf1.y, mf1.z, mf1.w};
+                        float key[4];
 #pragma unroll
-                    for (int u = 0; u < 4; ++u) {
-                        const int ci = 8 * g4 + 4 * h + u;  // code row of accumulator 4 g4 + u
-                        const int pop = __shfl(pc, ci) + __shfl(pc, ci + 32);
-                        const float f0 = __shfl(fr, ci), f1 = __shfl(fr, ci + 32);
-                        const int dot = acc[jb][4 * g4 + u] + off * pop;
-                        const float fd = __builtin_fmaf(c1, (float)dot, __builtin_fmaf(c2, (float)pop, -c34));
+                        for (int u = 0; u < 4; ++u) {
+                            // the oracle's order: fd = fmaf(c1, dot, fmaf(c2, pop, -c34)),
+                            // pre = fmaf(-2 f1, fd, f0 + qc), IP: 0.5 (pre - qn)
+                            const int dot = acc[jb][4 * g4 + u] + off * pa[u];
+                            const float fd = __builtin_fmaf(c1, (float)dot, __builtin_fmaf(c2, pfa[u], nc34));
+                            const float pre = __builtin_fmaf(m2f1[u], fd, __fadd_rn(f0a[u], qc));
+                            key[u] = IP ? __fmul_rn(0.5f, __fsub_rn(pre, qn)) : pre;
+                        }
                         if constexpr (SCREEN) {
-                            float key = rabitq_key(fd, f0, f1, qc, qn, ip);
-                            if (key != key) key = INFINITY;  // as the dense path's top-k
-                            const uint32_t id = scr.idbase + (uint32_t)(cb + ci);
-                            if (qok && ci < nc && pair_less(key, id, thd, thi)) {
-                                const int64_t slot = atomicAdd(scr.cnt + qa, 1u);
-                                scr.cand_d[qa * scr.ldc + slot] = key;
-                                scr.cand_i[qa * scr.ldc + slot] = id;
+                            // one compare per key; the exact (key, id) test (NaN -> +inf, ties by
+                            // id, the row and query guards) only for keys not above the threshold
+                            const bool any = !(key[0] > thd) || !(key[1] > thd) || !(key[2] > thd) || !(key[3] > thd);
+                            if (any) {
+#pragma unroll
+                                for (int u = 0; u < 4; ++u) {
+                                    const int ci = base + u;
+                                    const float kk = key[u] != key[u] ? INFINITY : key[u];
+                                    const uint32_t id = scr.idbase + (uint32_t)(cb + ci);
+                                    if (qok && ci < nc && pair_less(kk, id, thd, __float_as_uint(fb.w))) {
+                                        const int64_t slot = atomicAdd(scr.cnt + qa, 1u);
+                                        scr.cand_d[qa * scr.ldc + slot] = kk;
+                                        scr.cand_i[qa * scr.ldc + slot] = id;
+                                    }
+                                }
                             }
-                        } else if (qok && ci < nc) {
-                            orow[ci] = rabitq_key(fd, f0, f1, qc, qn, ip);
+                        } else {
+#pragma unroll
+                            for (int u = 0; u < 4; ++u)
+                                if (qok && base + u < nc) orow[base + u] = key[u];
                         }
                     }
                 }
-            }
+            };
+            if (ip) epilogue(std::true_type{});
+            else epilogue(std::false_type{});
         }
         if (c + 1 == nch) {
 #pragma unroll
@@ -637,7 +702,9 @@ extern "C" int mivq_rabitq_search(const uint8_t* codes, int64_t n, int32_t d, co
 #endif
     const int nqb_mq = nq > 64 ? 4 : nq > 32 ? 2 : 1;
     const bool mq = MIVQ_RQ_MQ && mfma && (d % kEstKC) == 0;
-    const size_t smem = mq ? (size_t)2 * 32 * nqb_mq * kEstQP : (size_t)32 * (d + 16);
+    // multi-query kernel: two staging stages, the per-query and per-wave epilogue terms
+    const size_t smem = mq ? (size_t)2 * 32 * nqb_mq * kEstQP + 32 * nqb_mq * 32 + kEstWaves * 512
+                           : (size_t)32 * (d + 16);
     if (mfma && smem > 160 * 1024) return set_error(MIVQ_ERR_UNSUPPORTED, "rabitq_search: d=%d too large", d);
     using MqFn = void (*)(const uint8_t*, int64_t, int, const int8_t*, const float*, int64_t, int, float*, unsigned,
                           RqScreen);

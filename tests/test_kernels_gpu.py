@@ -575,7 +575,7 @@ def test_rabitq_search_bit_exact(dev, oracle, nq, n, d, qb, k, metric):
 ])
 def test_rabitq_search_screened_blocks(dev, oracle, k, metric, order):
     """The screened search of the multi-query kernel (d % 512 == 0): a dense first block (two
-    column chunks of the tiled top-k at nq = 4100), then screened blocks whose keys are appended
+    column chunks of the tiled top-k at nq = 16500), then five screened blocks whose keys are appended
     only when they beat the query's running k-th element, merged in place.  Codes ordered so
     that query 0 finds a better code at every later position (its lists hold whole blocks),
     exact duplicates of first-block codes in later blocks (ties must keep the smaller id), a
@@ -583,7 +583,7 @@ def test_rabitq_search_screened_blocks(dev, oracle, k, metric, order):
     from haag_vq import _native
 
     rng = np.random.default_rng(k + metric)
-    nq, n, d = 4100, 40000, 512
+    nq, n, d = 16500, 40000, 512
     X = rng.standard_normal((n, d)).astype(np.float32)
     Q = rng.standard_normal((nq, d)).astype(np.float32)
     c = X.mean(0).astype(np.float32)
@@ -593,7 +593,7 @@ def test_rabitq_search_screened_blocks(dev, oracle, k, metric, order):
         keys0 = oracle.rabitq_est(codes, d, Q[:1], c, 4, metric)[0]
         codes = codes[np.argsort(-keys0, kind="stable")]
     dup_src = rng.choice(8000, 300, replace=False)
-    dup_dst = 16384 + rng.choice(n - 16384, 300, replace=False)
+    dup_dst = 8192 + rng.choice(n - 8192, 300, replace=False)
     codes[dup_dst] = codes[dup_src]
     codes = np.ascontiguousarray(codes)
     kd, ki = _native.rabitq_search(_t(codes, dev), d, cd, _t(Q, dev), 4, metric, k)

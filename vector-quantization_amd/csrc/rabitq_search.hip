@@ -429,8 +429,11 @@ __global__ __launch_bounds__(kEstWaves * 64) void rabitq_est_mq_kernel(
         // unconditional (the last step reloads rows it already has), so every wait is counted;
         // the staging half first: its mid-step store then waits for it alone, not for the
         // code bits issued after it
-        load_q(more ? cn : c, 0);
-        load_c(more ? crown : crow, more ? cn : c, cgn);
+#ifndef MIVQ_RQ_PROF
+#define MIVQ_RQ_PROF 0
+#endif
+        if (MIVQ_RQ_PROF != 2 && MIVQ_RQ_PROF != 3) load_q(more ? cn : c, 0);
+        if (MIVQ_RQ_PROF != 4) load_c(more ? crown : crow, more ? cn : c, cgn);
         __builtin_amdgcn_sched_barrier(0);  // issue them here (the scheduler sinks loads to their use)
         constexpr int ks = kEstKC / 32;  // k-steps per chunk (d % kEstKC == 0)
         const int8_t* qs = reinterpret_cast<const int8_t*>(smem + (it & 1) * STAGE) + r * kEstQP + 16 * h;
@@ -442,8 +445,10 @@ __global__ __launch_bounds__(kEstWaves * 64) void rabitq_est_mq_kernel(
         for (int gg = 0; gg < NG; ++gg) {
             {
                 if (gg == NG / 2) {  // mid-chunk: first staging half out, second in
+                    if (MIVQ_RQ_PROF != 2 && MIVQ_RQ_PROF != 3) {
                     store_q((int)((it + 1) & 1), 0);  // unconditional: the last step's copy is never read
                     load_q(more ? cn : c, 1);
+                    }
                     __builtin_amdgcn_sched_barrier(0);
                 }
 #pragma unroll
@@ -461,6 +466,7 @@ __global__ __launch_bounds__(kEstWaves * 64) void rabitq_est_mq_kernel(
                     v4i av;
 #pragma unroll
                     for (int j = 0; j < 4; ++j) av[j] = (int)(__umul24((b16 >> (4 * j)) & 0xFu, 0x204081u) & 0x01010101u);
+                    if (MIVQ_RQ_PROF == 6) av = (v4i){(int)cg[gg][u], (int)cg[gg][u] >> 1, (int)cg[gg][u] >> 2, (int)cg[gg][u] >> 3};
 #pragma unroll
                     for (int jb = 0; jb < NQB; ++jb) acc[jb] = __builtin_amdgcn_mfma_i32_32x32x32_i8(av, bq[jb], acc[jb], 0, 0, 0);
 #pragma unroll
@@ -468,7 +474,7 @@ __global__ __launch_bounds__(kEstWaves * 64) void rabitq_est_mq_kernel(
                 }
             }
         }
-        if (c + 1 == nch && nc > 0) {  // the group's last chunk: estimator epilogue (wave-uniform)
+        if (MIVQ_RQ_PROF != 1 && MIVQ_RQ_PROF != 5 && c + 1 == nch && nc > 0) {  // the group's last chunk: estimator epilogue (wave-uniform)
             const int64_t cb = (g * kEstWaves + w) * 32;
             const float fr = *reinterpret_cast<const float*>(crow + nb + 4 * h);  // h = 0: f0, 1: f1 of code r
             // per code r of the tile: pop (both k-halves), (float)pop, f0 and -2 f1 (exact), so that
@@ -543,15 +549,23 @@ __global__ __launch_bounds__(kEstWaves * 64) void rabitq_est_mq_kernel(
             if (ip) epilogue(std::true_type{});
             else epilogue(std::false_type{});
         }
+        if (MIVQ_RQ_PROF == 5 && c + 1 == nch) {  // profiling: the accumulators kept alive, no epilogue
+            int sum = pc;
+#pragma unroll
+            for (int jb = 0; jb < NQB; ++jb)
+#pragma unroll
+                for (int e = 0; e < 16; ++e) sum += acc[jb][e];
+            if (sum == 0x7FFFFFFF) buf[0] = 0.0f;
+        }
         if (c + 1 == nch) {
 #pragma unroll
             for (int jb = 0; jb < NQB; ++jb) acc[jb] = (v16i){};
             pc = 0;
         }
-        store_q((int)((it + 1) & 1), 1);
+        if (MIVQ_RQ_PROF != 2 && MIVQ_RQ_PROF != 3) store_q((int)((it + 1) & 1), 1);
 #pragma unroll
-        for (int gg = 0; gg < NG; ++gg) cg[gg] = cgn[gg];
-        lds_barrier();
+        for (int gg = 0; gg < NG; ++gg) cg[gg] = MIVQ_RQ_PROF == 4 ? cg[gg] : cgn[gg];
+        if (MIVQ_RQ_PROF != 3) lds_barrier();
         c = cn;
         g = gn;
         crow = crown;
@@ -634,11 +648,28 @@ __global__ __launch_bounds__(256) void rabitq_est_generic_kernel(const uint8_t* 
 }
 
 struct RqLayout {
-    size_t qq, qr, qf, tiled, cand_i, cnt, total;
+    size_t qq, qr, qf, tiled, cand_d, cand_i, cnt, total;
 };
 
-// The screened blocks' candidate keys reuse the tiled top-k's key block (nq x cols floats at the
-// start of its region); their ids and the per-query counts follow it.
+// Columns of the dense first block of the screened search: its top-k gives every query a
+// threshold (the k-th best of 8192 keys passes ~k / 8192 of the keys after it).
+constexpr int64_t kRqFirstCols = 8192;
+// Candidate-list entries (keys + ids, 8 B each) the screened blocks may use: a block is at most
+// 2^27 / nq codes wide (~134k at 1000 queries), so no list can overflow whatever the codes' order.
+constexpr int64_t kRqScreenEntries = (int64_t)1 << 27;
+
+// Width of the screened blocks (0: no screened block), whole 256-code groups.
+int64_t rq_screen_cols(int64_t nq, int64_t n) {
+    const int64_t rest = n - std::min<int64_t>(n, kRqFirstCols);
+    if (rest <= 0 || nq <= 0) return 0;
+    const int64_t g = kEstWaves * 32;
+    const int64_t w = std::max<int64_t>(16 * g, kRqScreenEntries / nq / g * g);
+    return std::min<int64_t>(w, ceil_div(rest, g) * g);
+}
+
+// Screened search (d % 512 == 0): the dense first block's tiled top-k region, then the candidate
+// lists (nq x rq_screen_cols keys and ids) and counts.  The dense search of other shapes uses the
+// same offset for its full tiled region (the two layouts never coexist in one call).
 RqLayout rq_layout(int64_t nq, int64_t n, int d, int k) {
     RqLayout L{};
     size_t off = 0;
@@ -646,16 +677,18 @@ RqLayout rq_layout(int64_t nq, int64_t n, int d, int k) {
     L.qq = off;    off = align_up(off + (size_t)nq * d, 256);
     L.qr = off;    off = align_up(off + (size_t)nq * d * 4, 256);
     L.qf = off;    off = align_up(off + (size_t)nq * kQfStride * 4, 256);
-    L.tiled = off; off = align_up(off + flat_tiled_workspace_bytes(nq, n, k), 256);
-    L.cand_i = off; off = align_up(off + (screened ? (size_t)nq * tiled_topk_cols(nq, n) * 4 : 0), 256);
-    L.cnt = off;   off = align_up(off + (screened ? (size_t)nq * 4 : 0), 256);
-    L.total = off;
+    L.tiled = off;
+    const size_t dense_all = align_up(off + flat_tiled_workspace_bytes(nq, n, k), 256);
+    if (screened) {
+        const size_t sc = (size_t)nq * rq_screen_cols(nq, n) * 4;
+        off = align_up(off + flat_tiled_workspace_bytes(nq, std::min<int64_t>(n, kRqFirstCols), k), 256);
+        L.cand_d = off; off = align_up(off + sc, 256);
+        L.cand_i = off; off = align_up(off + sc, 256);
+        L.cnt = off;    off = align_up(off + (size_t)nq * 4, 256);
+    }
+    L.total = std::max(off, dense_all);
     return L;
 }
-
-// Columns of the dense first block of the screened search: its top-k gives every query a
-// threshold (the k-th best of 16384 keys passes ~k / 16384 of the keys after it).
-constexpr int64_t kRqFirstCols = 16384;
 
 }  // namespace
 }  // namespace mivq
@@ -750,18 +783,19 @@ extern "C" int mivq_rabitq_search(const uint8_t* codes, int64_t n, int32_t d, co
             return hipGetLastError();
         });
     if (e == hipSuccess && n > n_dense) {
-        // screened blocks of about equal size (at most the key block's columns, whole 256-code
-        // groups), each followed by the merge of its candidates into (dists, ids)
-        const int64_t cap = tiled_topk_cols(nq, n);
-        const int64_t rest = n - n_dense;
-        const int64_t nblk = ceil_div(rest, cap);
-        const int64_t cols = std::min<int64_t>(cap, ceil_div(ceil_div(rest, nblk), kEstWaves * 32) * (kEstWaves * 32));
+        // screened blocks growing 4x from 4 x the first block (the threshold is refreshed after
+        // each: ~k x width / codes-so-far keys pass per query, and few queries' counters are
+        // contended when nq is small), capped at rq_screen_cols; whole 256-code groups; each
+        // followed by the merge of its candidates into (dists, ids)
+        const int64_t cap = rq_screen_cols(nq, n);
         uint32_t* cnt = reinterpret_cast<uint32_t*>(p + L.cnt);
-        RqScreen scr{dists, ids, k, cnt, reinterpret_cast<float*>(p + L.tiled),
+        RqScreen scr{dists, ids, k, cnt, reinterpret_cast<float*>(p + L.cand_d),
                      reinterpret_cast<uint32_t*>(p + L.cand_i), cap, 0u};
+        int64_t cols = std::min<int64_t>(cap, 4 * kRqFirstCols);
         e = hipMemsetAsync(cnt, 0, (size_t)nq * 4, st);
-        for (int64_t c0 = n_dense; c0 < n && e == hipSuccess; c0 += cols) {
-            const int64_t m = std::min<int64_t>(cols, n - c0);
+        for (int64_t c0 = n_dense, m = 0; c0 < n && e == hipSuccess; c0 += m, cols = std::min<int64_t>(cap, 4 * cols)) {
+            m = std::min<int64_t>(cols, n - c0);
+            if (n - c0 - m < cols / 4) m = std::min<int64_t>(cap, n - c0);  // no sliver of a last block
             scr.idbase = (uint32_t)(id_offset + c0);
             e = launch_mq(mq_screen, c0, m, nullptr, scr);
             if (e != hipSuccess) break;

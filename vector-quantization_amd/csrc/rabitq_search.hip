@@ -324,19 +324,12 @@ __global__ __launch_bounds__(kEstWaves * 64) void rabitq_est_mq_kernel(
     // persistent: workgroup b keeps query block b % nqb and walks the 256-code groups
     // b / nqb, + gridDim.x / nqb, ... (gridDim.x is a multiple of nqb), so the nqb workgroups of
     // a code group still run side by side (its code bits read from HBM once, then from L2)
-#ifndef MIVQ_RQ_XCD
-#define MIVQ_RQ_XCD 0
-#endif
-    unsigned qblk = blockIdx.x % nqb;
+    // (measured and not kept, profiles/r06_s14: the nqb workgroups of a code group placed on one
+    // XCD; static priority for waves 4-7 -- both 1.5 % slower)
+    const unsigned qblk = blockIdx.x % nqb;
     const int64_t gstep = gridDim.x / nqb;
     const int64_t ngroups = (m + kEstWaves * 32 - 1) / (kEstWaves * 32);
-    int64_t g0 = blockIdx.x / nqb;
-    if (MIVQ_RQ_XCD && gridDim.x % (8 * nqb) == 0) {
-        // the nqb workgroups of a code group on one XCD (blocks b and b + 8 share one)
-        const unsigned x = blockIdx.x % 8, j = blockIdx.x / 8;
-        qblk = j % nqb;
-        g0 = x + 8 * (j / nqb);
-    }
+    const int64_t g0 = blockIdx.x / nqb;
     const int64_t q0 = (int64_t)qblk * QR;
     const int nb = d >> 3, cs = nb + 8;
     const int nch = d / kEstKC;  // d % kEstKC == 0 (host)
@@ -414,10 +407,6 @@ __global__ __launch_bounds__(kEstWaves * 64) void rabitq_est_mq_kernel(
         store_q(0, 1);
     }
     lds_barrier();
-#ifndef MIVQ_RQ_PRIO
-#define MIVQ_RQ_PRIO 0
-#endif
-    if (MIVQ_RQ_PRIO && w >= kEstWaves / 2) __builtin_amdgcn_s_setprio(1);
     for (int64_t it = 0; it < nit; ++it) {
         // the next step's chunk (the next group's first one at the end of a group)
         const bool more = it + 1 < nit;  // uniform
@@ -429,15 +418,13 @@ __global__ __launch_bounds__(kEstWaves * 64) void rabitq_est_mq_kernel(
         // unconditional (the last step reloads rows it already has), so every wait is counted;
         // the staging half first: its mid-step store then waits for it alone, not for the
         // code bits issued after it
-#ifndef MIVQ_RQ_PROF
-#define MIVQ_RQ_PROF 0
-#endif
-        if (MIVQ_RQ_PROF != 2 && MIVQ_RQ_PROF != 3) load_q(more ? cn : c, 0);
-        if (MIVQ_RQ_PROF != 4) load_c(more ? crown : crow, more ? cn : c, cgn);
+        load_q(more ? cn : c, 0);
+        load_c(more ? crown : crow, more ? cn : c, cgn);
         __builtin_amdgcn_sched_barrier(0);  // issue them here (the scheduler sinks loads to their use)
         constexpr int ks = kEstKC / 32;  // k-steps per chunk (d % kEstKC == 0)
         const int8_t* qs = reinterpret_cast<const int8_t*>(smem + (it & 1) * STAGE) + r * kEstQP + 16 * h;
         // the B operands (query bytes) of k-step s + 1 are read from LDS while step s's MFMAs run
+        // (B reads two k-steps ahead: 1 % slower, profiles/r06_s21)
         v4i bq[NQB];
 #pragma unroll
         for (int jb = 0; jb < NQB; ++jb) bq[jb] = *reinterpret_cast<const v4i*>(qs + jb * 32 * kEstQP);
@@ -445,10 +432,8 @@ __global__ __launch_bounds__(kEstWaves * 64) void rabitq_est_mq_kernel(
         for (int gg = 0; gg < NG; ++gg) {
             {
                 if (gg == NG / 2) {  // mid-chunk: first staging half out, second in
-                    if (MIVQ_RQ_PROF != 2 && MIVQ_RQ_PROF != 3) {
                     store_q((int)((it + 1) & 1), 0);  // unconditional: the last step's copy is never read
                     load_q(more ? cn : c, 1);
-                    }
                     __builtin_amdgcn_sched_barrier(0);
                 }
 #pragma unroll
@@ -466,7 +451,6 @@ __global__ __launch_bounds__(kEstWaves * 64) void rabitq_est_mq_kernel(
                     v4i av;
 #pragma unroll
                     for (int j = 0; j < 4; ++j) av[j] = (int)(__umul24((b16 >> (4 * j)) & 0xFu, 0x204081u) & 0x01010101u);
-                    if (MIVQ_RQ_PROF == 6) av = (v4i){(int)cg[gg][u], (int)cg[gg][u] >> 1, (int)cg[gg][u] >> 2, (int)cg[gg][u] >> 3};
 #pragma unroll
                     for (int jb = 0; jb < NQB; ++jb) acc[jb] = __builtin_amdgcn_mfma_i32_32x32x32_i8(av, bq[jb], acc[jb], 0, 0, 0);
 #pragma unroll
@@ -474,7 +458,7 @@ __global__ __launch_bounds__(kEstWaves * 64) void rabitq_est_mq_kernel(
                 }
             }
         }
-        if (MIVQ_RQ_PROF != 1 && MIVQ_RQ_PROF != 5 && c + 1 == nch && nc > 0) {  // the group's last chunk: estimator epilogue (wave-uniform)
+        if (c + 1 == nch && nc > 0) {  // the group's last chunk: estimator epilogue (wave-uniform)
             const int64_t cb = (g * kEstWaves + w) * 32;
             const float fr = *reinterpret_cast<const float*>(crow + nb + 4 * h);  // h = 0: f0, 1: f1 of code r
             // per code r of the tile: pop (both k-halves), (float)pop, f0 and -2 f1 (exact), so that
@@ -549,23 +533,15 @@ __global__ __launch_bounds__(kEstWaves * 64) void rabitq_est_mq_kernel(
             if (ip) epilogue(std::true_type{});
             else epilogue(std::false_type{});
         }
-        if (MIVQ_RQ_PROF == 5 && c + 1 == nch) {  // profiling: the accumulators kept alive, no epilogue
-            int sum = pc;
-#pragma unroll
-            for (int jb = 0; jb < NQB; ++jb)
-#pragma unroll
-                for (int e = 0; e < 16; ++e) sum += acc[jb][e];
-            if (sum == 0x7FFFFFFF) buf[0] = 0.0f;
-        }
         if (c + 1 == nch) {
 #pragma unroll
             for (int jb = 0; jb < NQB; ++jb) acc[jb] = (v16i){};
             pc = 0;
         }
-        if (MIVQ_RQ_PROF != 2 && MIVQ_RQ_PROF != 3) store_q((int)((it + 1) & 1), 1);
+        store_q((int)((it + 1) & 1), 1);
 #pragma unroll
-        for (int gg = 0; gg < NG; ++gg) cg[gg] = MIVQ_RQ_PROF == 4 ? cg[gg] : cgn[gg];
-        if (MIVQ_RQ_PROF != 3) lds_barrier();
+        for (int gg = 0; gg < NG; ++gg) cg[gg] = cgn[gg];
+        lds_barrier();
         c = cn;
         g = gn;
         crow = crown;

@@ -62,6 +62,7 @@ SETTLE_MS = 60.0               # untimed busy time after the W warmup calls of a
 MFMA_F32_PEAK_TFS = 157.3      # dense fp32 matrix peak (same table)
 MFMA_F16_PEAK_TFS = 2516.6     # dense f16/bf16 matrix peak = 16 x fp32 (same table)
 MFMA_F64_PEAK_TFS = 78.6       # dense fp64 matrix peak (MI355X spec; not in the guide's table)
+INT8_MFMA_PEAK_TOPS = 2 * MFMA_F16_PEAK_TFS  # v_mfma_i32_32x32x32_i8: the cycles of the f16 32x32x16 at 2x K
 LDS_PEAK_GBS = 256 * 256 * 2.4  # 256 CUs x 256 B/clk (ds_read_b128) x 2.4 GHz = 157 TB/s
 # The filtered ADC scan (adc_qscan_kernel) is VALU-issue bound (its LDS reads are
 # conflict-free since round 6 and PMC shows the VALU pipe saturated, profiles/r06_s1/pmc_*).
@@ -541,9 +542,17 @@ def flatcodes_leg(a, dev, kind, steps, warmup, cpu=True):
         est = lambda: _native.rabitq_search(codes_c, d, center, Qe, 4, _native.METRIC_L2, 10)  # noqa: E731
         ewall, _ = timed(est, 3, 1)
         _, ei = est()
+        # the integer dots <bits, q'> of every (query, code) pair on v_mfma_i32_32x32x32_i8: 2 d ops
+        # per pair over the whole search (query prep, first-block top-k and merges included)
+        tops = 2.0 * a.nq * n * d / ewall / 1e12
         out["estimator_search"] = {"qps": a.nq / ewall, "nq": a.nq, "k": 10, "qb": 4, "ms_per_batch": ewall * 1e3,
                                    "recall@10": rec(g_, ei[:100].cpu().numpy()),
-                                   "method": "mivq_rabitq_search: int8 MFMA over sign bits + estimator + tiled top-k"}
+                                   "roofline": {"bound": "mfma", "achieved": tops, "peak": INT8_MFMA_PEAK_TOPS,
+                                                "unit": "TOPS", "frac": tops / INT8_MFMA_PEAK_TOPS,
+                                                "ops_per_pair": 2 * d},
+                                   "method": "mivq_rabitq_search: int8 MFMA over sign bits (128 queries per "
+                                             "workgroup) + estimator; dense first block + tiled top-k, then "
+                                             "screened blocks (keys kept only below the running k-th) merged in place"}
     if cpu:
         out["cpu_baseline"] = flatcodes_cpu_baseline(kind, X, codes, lo if kind == "sq8" else None,
                                                      den if kind == "sq8" else None, a.cpu_seconds / 2)
@@ -771,6 +780,10 @@ def summary_of(out, k):
     for name, leg in cf.items():
         if isinstance(leg, dict):
             sm[name] = {"value": r(leg.get("value"), 0), "frac": r((leg.get("roofline") or {}).get("frac"))}
+            es = leg.get("estimator_search")
+            if es:
+                sm[name]["estimator_qps"] = r(es["qps"], 0)
+                sm[name]["estimator_frac"] = r((es.get("roofline") or {}).get("frac"))
     return sm
 
 

@@ -704,7 +704,7 @@ __device__ __forceinline__ uint32_t umed3(uint32_t a, uint32_t b, uint32_t c) {
     return r;
 }
 
-template <int MC>
+template <int MC, bool PIN>
 __global__ __launch_bounds__(kScanWaves * 64) void adc_qscan_kernel(
     const uint32_t* __restrict__ qtab, int64_t nq, const uint8_t* __restrict__ codes, int64_t n, int k1,
     int64_t id_offset, int64_t chunk_rows, float* __restrict__ part_d, uint32_t* __restrict__ part_i,
@@ -775,16 +775,17 @@ __global__ __launch_bounds__(kScanWaves * 64) void adc_qscan_kernel(
     int voffc[4];
 #pragma unroll
     for (int i = 0; i < 4; ++i) voffc[i] = (wv * 64 + lane) * (16 * MC) + 4 * (int)((i + rd) & 3u);
-    auto fetchb = [&](int64_t base) __attribute__((always_inline)) {
+    auto fetchb_to = [&](int64_t base, uint4 (&dst)[MC]) __attribute__((always_inline)) {
         const int so = (int)(base - rbeg) * (16 * MC);
 #pragma unroll
         for (int c = 0; c < MC; ++c) {
-            cw[c].x = __builtin_amdgcn_raw_buffer_load_b32(crs, voffc[0], so + 16 * c, 0);
-            cw[c].y = __builtin_amdgcn_raw_buffer_load_b32(crs, voffc[1], so + 16 * c, 0);
-            cw[c].z = __builtin_amdgcn_raw_buffer_load_b32(crs, voffc[2], so + 16 * c, 0);
-            cw[c].w = __builtin_amdgcn_raw_buffer_load_b32(crs, voffc[3], so + 16 * c, 0);
+            dst[c].x = __builtin_amdgcn_raw_buffer_load_b32(crs, voffc[0], so + 16 * c, 0);
+            dst[c].y = __builtin_amdgcn_raw_buffer_load_b32(crs, voffc[1], so + 16 * c, 0);
+            dst[c].z = __builtin_amdgcn_raw_buffer_load_b32(crs, voffc[2], so + 16 * c, 0);
+            dst[c].w = __builtin_amdgcn_raw_buffer_load_b32(crs, voffc[3], so + 16 * c, 0);
         }
     };
+    auto fetchb = [&](int64_t base) __attribute__((always_inline)) { fetchb_to(base, cw); };
     // the code row's dwords rotated by rd within each 16-B half (two select levels)
     auto rot = [&](uint4 w) __attribute__((always_inline)) {
         const bool r1 = (rd & 1u) != 0u, r2 = (rd & 2u) != 0u;
@@ -809,6 +810,11 @@ __global__ __launch_bounds__(kScanWaves * 64) void adc_qscan_kernel(
         for (int c = 0; c < MC; ++c) cur[c] = cw[c];
         if constexpr (kBuf) fetchb(base - (int64_t)wv * 64 + kScanWaves * 64);
         else fetch(row + kScanWaves * 64);
+        // PIN (round 6): the next row's loads issue here, at the top of the step, so they have the
+        // whole step to land (the compiler otherwise places them ~30 % into it, and the copy at
+        // the loop latch waits for them): 8 % faster at the config #5 shape, 2 % slower when one
+        // round of workgroups covers the search (1000 x 1M), so launch_qscan picks it by shape
+        if constexpr (PIN) __builtin_amdgcn_sched_barrier(0);
         uint32_t wq[4 * MC];
 #pragma unroll
         for (int c = 0; c < MC; ++c) {
@@ -1177,7 +1183,12 @@ template <int MC>
 hipError_t launch_qscan(const uint32_t* tab, int64_t nq, const uint8_t* codes, int64_t n, int k1, int64_t id_offset,
                         const AdcFilteredLayout& L, float* p1d, uint32_t* p1i, float* p1b, hipStream_t st) {
     constexpr int M = 16 * MC;
-    auto kern = adc_qscan_kernel<MC>;
+    // the pinned prefetch when the workgroups take more than one round of the chip's CUs
+#ifndef MIVQ_QSCAN_PIN_MODE
+#define MIVQ_QSCAN_PIN_MODE 2  // 0: never, 1: always, 2: by shape
+#endif
+    const bool pin = MIVQ_QSCAN_PIN_MODE == 1 || (MIVQ_QSCAN_PIN_MODE == 2 && L.nch * ceil_div(nq, kQB) > 256);
+    auto kern = pin ? adc_qscan_kernel<MC, true> : adc_qscan_kernel<MC, false>;
     const int smem = M * 256 * kQB;
     const hipError_t e = hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, smem);
     if (e != hipSuccess) return e;

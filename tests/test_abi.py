@@ -105,6 +105,22 @@ def test_adc_search_workspace_bounded():
     assert 0 < nb < 3 * 2 ** 30, nb
 
 
+def test_rabitq_search_workspace_bounded():
+    """The screened estimator search's candidate lists (keys + ids, worst case every key of a
+    block) are capped at 2^27 entries (1 GiB) per block, and its dense first block needs only
+    8,192 columns: at 1,000 queries x 1M codes x 3072 the whole workspace stays near 1.1 GiB
+    (the pre-screen tiled search alone held a 256 MiB key block), and at 100,000 queries it is
+    dominated by the per-query int8 / fp32 rows, not by the lists."""
+    from haag_vq import _native
+
+    lib = _native.load_library()
+    nb = lib.mivq_rabitq_search_workspace_bytes(1000, 1_000_000, 3072, 10)
+    assert 0 < nb < 1.25 * 2 ** 30, nb
+    nb = lib.mivq_rabitq_search_workspace_bytes(100_000, 10_000_000, 3072, 10)
+    rows = 100_000 * 3072 * 5  # qq (int8) + qr (fp32) rows
+    assert 0 < nb < rows + 3 * 2 ** 30, nb
+
+
 def test_qscan_valu_counts_match_bench():
     """bench.py prices the filtered ADC scan's roofline from the static VALU count of one
     wave-step of adc_qscan_kernel (QSCAN_VALU_PER_STEP); that count must be the built library's."""

@@ -639,7 +639,7 @@ int64_t rq_screen_cols(int64_t nq, int64_t n) {
     const int64_t rest = n - std::min<int64_t>(n, kRqFirstCols);
     if (rest <= 0 || nq <= 0) return 0;
     const int64_t g = kEstWaves * 32;
-    const int64_t w = std::max<int64_t>(16 * g, kRqScreenEntries / nq / g * g);
+    const int64_t w = std::max<int64_t>(4 * g, kRqScreenEntries / nq / g * g);  // >= 1024 codes
     return std::min<int64_t>(w, ceil_div(rest, g) * g);
 }
 

@@ -1151,6 +1151,22 @@ int adc_k1(int k) { return k + kListSlack; }
 bool adc_filtered_shape(int M, int ksub, int k) { return ksub == 256 && (M == 16 || M == 32) && k <= 32; }
 int adc_fqb(int M, int k) { return kQB; }
 
+// Row chunks of the filtered (integer) scan: the cost model's, then, when its grid fits one round
+// of the CUs, at least 4 chunks and at most 1024 wave-steps per chunk (the grid then takes several
+// rounds and launch_qscan the pinned-prefetch kernel).  Measured (round 6, profiles/r06_s30, 1M
+// rows unless noted; results identical): 2000 queries 0.99 -> 0.79 ms, 4000 queries 1.77 ->
+// 1.44 ms, 1000 x 6.65M 2.65 -> 2.20 ms, 3000 x 6.65M 6.57 -> 6.18 ms, while 500 / 1000 queries
+// over 1M-4M rows (model already at 4+ chunks, <= 1024 steps) and the multi-round config #5 grid
+// keep the model's count (more chunks there measured 1-17 % slower).
+int64_t adc_qscan_chunks(int64_t nq, int64_t n, int QB) {
+    int64_t nch = adc_chunks(nq, n, QB);
+    const int64_t qblocks = ceil_div(nq, QB), step_rows = 64 * kScanWaves;
+    const int64_t most = std::max<int64_t>(1, std::min<int64_t>(1024, ceil_div(n, step_rows)));
+    if (nch * qblocks <= 256)
+        while (nch < most && (nch < 4 || ceil_div(ceil_div(n, nch), step_rows) > 1024)) nch = std::min(most, 2 * nch);
+    return nch;
+}
+
 struct AdcFilteredLayout {
     size_t stats, mins, tab, p1d, p1i, p1b, fail, total;
     int64_t nch, parts;
@@ -1166,7 +1182,7 @@ AdcFilteredLayout adc_filtered_layout(int64_t nq, int64_t n, int M, int k, size_
     // most 65535 wave-steps (of 1024 rows) per chunk
     const size_t per_chunk = (size_t)kScanWaves * (size_t)nq * (size_t)L.k1 * 8u;
     const int64_t cap = std::max<int64_t>(1, (int64_t)((size_t(1) << 30) / per_chunk));
-    L.nch = std::max<int64_t>(std::min<int64_t>(adc_chunks(nq, n, QB), cap), ceil_div(n, (int64_t)65535 * kScanWaves * 64));
+    L.nch = std::max<int64_t>(std::min<int64_t>(adc_qscan_chunks(nq, n, QB), cap), ceil_div(n, (int64_t)65535 * kScanWaves * 64));
     L.parts = L.nch * kScanWaves;
     L.stats = off;  off = align_up(off + (size_t)nq * sizeof(AdcQStat), 256);
     L.mins = off;   off = align_up(off + (size_t)nq * M * sizeof(float), 256);

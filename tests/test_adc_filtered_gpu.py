@@ -157,3 +157,28 @@ def test_filtered_adc_rerun_many_slot_blocks_large_db(dev):
         np.testing.assert_array_equal(i_f[q], _h(order).astype(np.uint32) + 11)
         np.testing.assert_array_equal(d_f[q], _h(dist[order]))
 
+
+
+@pytest.mark.parametrize("nq,n", [(4200, 30_000), (2000, 200_000)])
+def test_filtered_adc_grid_shapes(dev, nq, n):
+    """Grids of more than one round of CUs: 4200 queries (263 query blocks x 1 chunk) take the
+    pinned-prefetch scan kernel; 2000 queries over 200k rows take the one-round chunk rule
+    (2 -> 4 chunks, then two rounds, pinned).  Equal to the fp32 scan for every query and to a
+    torch restatement of the canonical sums for a few."""
+    g = torch.Generator(device=dev).manual_seed(nq)
+    M, k = 16, 10
+    codes = torch.randint(0, 256, (n, M), device=dev, dtype=torch.uint8, generator=g)
+    codes[n - 1] = codes[3]  # a duplicate row: tie to the smaller id
+    lut = torch.rand((nq, M, 256), device=dev, generator=g, dtype=torch.float32)
+    d_f, i_f = _search(lut, codes, k, 5)
+    d_e, i_e = _search(lut, codes, k, 5, EXACT)
+    np.testing.assert_array_equal(d_f, d_e)
+    np.testing.assert_array_equal(i_f, i_e)
+    ci = codes.long()
+    for q in (0, nq // 2, nq - 1):
+        dist = lut[q, 0][ci[:, 0]].clone()
+        for m in range(1, M):
+            dist += lut[q, m][ci[:, m]]
+        order = torch.sort(dist, stable=True).indices[:k]
+        np.testing.assert_array_equal(i_f[q], _h(order).astype(np.uint32) + 5)
+        np.testing.assert_array_equal(d_f[q], _h(dist[order]))

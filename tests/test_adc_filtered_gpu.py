@@ -159,14 +159,14 @@ def test_filtered_adc_rerun_many_slot_blocks_large_db(dev):
 
 
 
-@pytest.mark.parametrize("nq,n", [(4200, 30_000), (2000, 200_000)])
-def test_filtered_adc_grid_shapes(dev, nq, n):
+@pytest.mark.parametrize("nq,n,M", [(4200, 30_000, 16), (2000, 200_000, 16), (4200, 30_000, 32)])
+def test_filtered_adc_grid_shapes(dev, nq, n, M):
     """Grids of more than one round of CUs: 4200 queries (263 query blocks x 1 chunk) take the
-    pinned-prefetch scan kernel; 2000 queries over 200k rows take the one-round chunk rule
-    (2 -> 4 chunks, then two rounds, pinned).  Equal to the fp32 scan for every query and to a
+    pinned-prefetch scan kernel (M = 16 and M = 32); 2000 queries over 200k rows take the
+    one-round chunk rule (2 -> 4 chunks, then two rounds, pinned).  Equal to the fp32 scan for every query and to a
     torch restatement of the canonical sums for a few."""
-    g = torch.Generator(device=dev).manual_seed(nq)
-    M, k = 16, 10
+    g = torch.Generator(device=dev).manual_seed(nq + M)
+    k = 10
     codes = torch.randint(0, 256, (n, M), device=dev, dtype=torch.uint8, generator=g)
     codes[n - 1] = codes[3]  # a duplicate row: tie to the smaller id
     lut = torch.rand((nq, M, 256), device=dev, generator=g, dtype=torch.float32)

@@ -57,8 +57,10 @@ def main_loop(ins):
 def count(lib: Path) -> dict:
     txt = isa_audit.disassemble(lib)
     res = {}
-    for mc, m in ((1, 16), (2, 32)):
-        body = main_loop(kernel_lines(txt, f"adc_qscan_kernelILi{mc}E"))
+    # the variants the product runs: M = 16 unpinned (the pinned one has the same count), M = 32
+    # pinned (launch_qscan always takes it at M = 32, with the buffer-loaded code rows)
+    for mc, m, pin in ((1, 16, 0), (2, 32, 1)):
+        body = main_loop(kernel_lines(txt, f"adc_qscan_kernelILi{mc}ELb{pin}E"))
         valu = [x for x in body if x[0].startswith("v_")]
         res[str(m)] = {"valu": len(valu), "valu_32bit": sum(1 for x in valu if x[3] == 1),
                        "valu_64bit": sum(1 for x in valu if x[3] >= 2),

@@ -769,7 +769,13 @@ __global__ __launch_bounds__(kScanWaves * 64) void adc_qscan_kernel(
     // and the wave-step in the scalar soffset, range-checked over the chunk (rows past it read
     // zeros), so neither the rotation nor the row address costs VALU.  (M = 32: the select
     // rotation below; eight such loads per row spilled there.)
-    constexpr bool kBuf = MIVQ_QSCAN_BUF && MC == 1;
+    // (M = 32: the buffer path in the pinned kernel only -- the unpinned one spills with it --
+    // and launch_qscan always takes the pinned kernel at M = 32: 2-3 % faster at 1000 / 4000 x 1M
+    // and 10,000 x 6.65M, profiles/r06_s34)
+#ifndef MIVQ_QSCAN_M32BUF
+#define MIVQ_QSCAN_M32BUF 1
+#endif
+    constexpr bool kBuf = MIVQ_QSCAN_BUF && (MC == 1 || (MIVQ_QSCAN_M32BUF && MC == 2 && PIN));
     const __amdgpu_buffer_rsrc_t crs = __builtin_amdgcn_make_buffer_rsrc(
         (void*)(codes + rbeg * (16 * MC)), 0, (int)(max<int64_t>(0, rend - rbeg) * (16 * MC)), 0x00020000);
     int voffc[4];
@@ -1203,7 +1209,8 @@ hipError_t launch_qscan(const uint32_t* tab, int64_t nq, const uint8_t* codes, i
 #ifndef MIVQ_QSCAN_PIN_MODE
 #define MIVQ_QSCAN_PIN_MODE 2  // 0: never, 1: always, 2: by shape
 #endif
-    const bool pin = MIVQ_QSCAN_PIN_MODE == 1 || (MIVQ_QSCAN_PIN_MODE == 2 && L.nch * ceil_div(nq, kQB) > 256);
+    const bool pin = MIVQ_QSCAN_PIN_MODE == 1 || (MIVQ_QSCAN_PIN_MODE == 2 && L.nch * ceil_div(nq, kQB) > 256) ||
+                     (MIVQ_QSCAN_M32BUF && MC == 2);
     auto kern = pin ? adc_qscan_kernel<MC, true> : adc_qscan_kernel<MC, false>;
     const int smem = M * 256 * kQB;
     const hipError_t e = hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, smem);

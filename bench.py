@@ -69,7 +69,7 @@ LDS_PEAK_GBS = 256 * 256 * 2.4  # 256 CUs x 256 B/clk (ds_read_b128) x 2.4 GHz =
 # Its roofline is the chip's VALU issue rate for its instruction mix: the static count of one
 # wave-step (64 rows x 16 queries) of the built kernel, split by encoding (tools/isa_qscan.py,
 # checked against the library by tests/test_abi.py) ...
-QSCAN_VALU_PER_STEP = {16: {"valu_32bit": 48, "valu_64bit": 122}, 32: {"valu_32bit": 67, "valu_64bit": 219}}
+QSCAN_VALU_PER_STEP = {16: {"valu_32bit": 64, "valu_64bit": 106}, 32: {"valu_32bit": 99, "valu_64bit": 187}}
 # ... priced at the issue rates tools/probes/valu_rate.hip measured with 4 waves per SIMD on every
 # CU (chip wave-instructions/s under that load; profiles/r06_s5/valu_rate.log): 32-bit-encoded
 # VALU (v_add_u32_e32) 0.881e12, 64-bit-encoded VALU (v_perm_b32 / v_med3_u32 / v_lshl_or_b32,

@@ -567,6 +567,8 @@ struct AdcQStat {
 // (5 bits, eight lookups per unpack: 3-5 % faster on clustered rows and the config #5 shape, but
 // 1.6x slower on 1M x 1536 Gaussian rows, whose queries it mostly fails to certify; r05_s22)
 constexpr int kAdcBits = 6;
+// (round 6, with the scan VALU-bound: 2 keys -- one v_med3 less per row and query -- measured
+// 2.4x / 1.23x slower at 1000 x 1M / the config #5 shape: the uncertified queries' fp32 re-runs)
 constexpr int kLaneKeys = 3;
 constexpr double kAdcSpan = 2.0;  // the grid's span in mean offsets above the minimum
 __host__ __device__ constexpr int adc_qmax(int) { return (1 << kAdcBits) - 1; }
@@ -776,6 +778,11 @@ __global__ __launch_bounds__(kScanWaves * 64) void adc_qscan_kernel(
 #define MIVQ_QSCAN_M32BUF 1
 #endif
     constexpr bool kBuf = MIVQ_QSCAN_BUF && (MC == 1 || (MIVQ_QSCAN_M32BUF && MC == 2 && PIN));
+    // the even-query unpack (bytes 0 and 2 -> the u16 pair) is a mask: with the mask in an SGPR it
+    // is a 32-bit v_and instead of a 64-bit v_perm (the scan is VALU-issue bound, DESIGN 3.3;
+    // 1.2-1.5 % faster at M = 16 / 32, 1000 x 1M and the config #5 shape, profiles/r06_s35)
+    uint32_t mlo;
+    asm volatile("s_mov_b32 %0, 0xff00ff" : "=s"(mlo));
     const __amdgpu_buffer_rsrc_t crs = __builtin_amdgcn_make_buffer_rsrc(
         (void*)(codes + rbeg * (16 * MC)), 0, (int)(max<int64_t>(0, rend - rbeg) * (16 * MC)), 0x00020000);
     int voffc[4];
@@ -848,7 +855,7 @@ __global__ __launch_bounds__(kScanWaves * 64) void adc_qscan_kernel(
                 if ((4 * jw + b + 1) % UNP == 0) {
 #pragma unroll
                     for (int wd = 0; wd < 4; ++wd) {  // bytes (4w, 4w+2, 4w+1, 4w+3) -> u16 pairs
-                        acc[2 * wd] += __builtin_amdgcn_perm(a8[wd], a8[wd], 0x0C020C00u);
+                        acc[2 * wd] += a8[wd] & mlo;
                         acc[2 * wd + 1] += __builtin_amdgcn_perm(a8[wd], a8[wd], 0x0C030C01u);
                     }
                 }

@@ -319,9 +319,13 @@ def cpu_baseline(X, C, O, target_s):
 
 
 # ------------------------------------------------------------------------- ADC
-def adc_leg(X, C, codes, a, rank, world, dev, Q, k, gt_queries, reps=10, cpu=True):
+def adc_leg(X, C, codes, a, rank, world, dev, Q, k, gt_queries, reps=30, cpu=True):
     """Sharded ADC search + its roofline + the reference's decode-then-exact ranking on the
-    same codes (+ the oracle's ADC on the host cores at N = 1)."""
+    same codes (+ the oracle's ADC on the host cores at N = 1).
+
+    reps: 30 calls of ~0.45 ms at 1000 x 1M (10 calls, a 5 ms timed region, read ~6 % slow: the
+    host's first enqueue and the final synchronize are not amortised; tools/probe_adc_wall.py,
+    profiles/r06_s37); the 20 ms config #5 calls take 2."""
     nbits = 8
     n, d = X.shape
     M = C.shape[0]

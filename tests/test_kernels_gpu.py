@@ -403,8 +403,10 @@ def test_rabitq_parity_with_centroid(dev, oracle, n, d):
 
 
 @pytest.mark.parametrize("nq,n,d,M,nbits,k", [
-    (37, 5000, 1536, 16, 8, 10),
-    (9, 3000, 1536, 32, 8, 100),
+    (37, 5000, 1536, 16, 8, 10),    # LUT: compile-time dsub 96
+    (9, 3000, 1536, 32, 8, 100),    # dsub 48
+    (11, 2000, 1024, 16, 8, 10),    # dsub 64
+    (13, 700, 256, 2, 8, 10),       # packed LUT kernel, run-time dsub (128)
     (16, 1000, 64, 8, 4, 7),
     (5, 200, 48, 6, 8, 256),
     (3, 5, 64, 8, 8, 10),   # fewer rows than k: sentinel slots

@@ -100,7 +100,7 @@ __global__ __launch_bounds__(256) void adc_lut_kernel(const float* __restrict__ 
 // so no packed instruction reads an LDS-loaded register.  Half the VALU of the
 // scalar kernel, and no LDS reads at all.
 constexpr int kLutPkQ = 8;
-template <bool L2>
+template <bool L2, int DS>
 __global__ __launch_bounds__(128) void adc_lut_pk_kernel(const float* __restrict__ q, int64_t nq, int d, int M,
                                                           int dsub, const float* __restrict__ C,
                                                           float* __restrict__ lut) {
@@ -116,15 +116,7 @@ __global__ __launch_bounds__(128) void adc_lut_pk_kernel(const float* __restrict
     float2v acc[kLutPkQ];
 #pragma unroll
     for (int qq = 0; qq < kLutPkQ; ++qq) acc[qq] = (float2v){0.0f, 0.0f};
-    v4f a = *reinterpret_cast<const v4f*>(ca), b = *reinterpret_cast<const v4f*>(cb);
-#ifndef MIVQ_LUT_UNROLL
-#define MIVQ_LUT_UNROLL 1
-#endif
-#pragma unroll MIVQ_LUT_UNROLL
-    for (int t0 = 0; t0 < dsub; t0 += 4) {
-        const bool more = t0 + 4 < dsub;
-        const v4f an = more ? *reinterpret_cast<const v4f*>(ca + t0 + 4) : a;
-        const v4f bn = more ? *reinterpret_cast<const v4f*>(cb + t0 + 4) : b;
+    auto body = [&](const v4f& a, const v4f& b, int t0) __attribute__((always_inline)) {
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
             const float2v cc = {a[j], b[j]};
@@ -140,8 +132,30 @@ __global__ __launch_bounds__(128) void adc_lut_pk_kernel(const float* __restrict
                 }
             }
         }
+    };
+    if constexpr (DS > 0) {
+        // compile-time dsub: both centroid rows are loaded up front (DS / 2 16-B loads per thread,
+        // all in flight at once) and consumed in order as they land, instead of one 16-B step
+        // ahead with a wait at every loop latch
+        // (a window of W steps ahead instead spills: the scheduler hoists every load regardless)
+        v4f ra[DS / 4], rb[DS / 4];
+#pragma unroll
+        for (int i = 0; i < DS / 4; ++i) {
+            ra[i] = *reinterpret_cast<const v4f*>(ca + 4 * i);
+            rb[i] = *reinterpret_cast<const v4f*>(cb + 4 * i);
+        }
+#pragma unroll
+        for (int i = 0; i < DS / 4; ++i) body(ra[i], rb[i], 4 * i);
+    } else {
+    v4f a = *reinterpret_cast<const v4f*>(ca), b = *reinterpret_cast<const v4f*>(cb);
+    for (int t0 = 0; t0 < dsub; t0 += 4) {
+        const bool more = t0 + 4 < dsub;
+        const v4f an = more ? *reinterpret_cast<const v4f*>(ca + t0 + 4) : a;
+        const v4f bn = more ? *reinterpret_cast<const v4f*>(cb + t0 + 4) : b;
+        body(a, b, t0);
         a = an;
         b = bn;
+    }
     }
 #pragma unroll
     for (int qq = 0; qq < kLutPkQ; ++qq) {
@@ -1362,12 +1376,22 @@ extern "C" int mivq_adc_lut(const float* q, int64_t nq, int32_t d, int32_t M, in
 #endif
     if (MIVQ_LUT_PK && ksub == 256 && (d / M) % 4 == 0 && reinterpret_cast<uintptr_t>(centroids) % 16 == 0) {
         const dim3 grid((unsigned)M, (unsigned)ceil_div(nq, kLutPkQ));
-        if (metric == MIVQ_METRIC_L2)
-            hipLaunchKernelGGL(adc_lut_pk_kernel<true>, grid, dim3(128), 0, as_stream(stream), q, nq, d, M, d / M,
-                               centroids, lut);
-        else
-            hipLaunchKernelGGL(adc_lut_pk_kernel<false>, grid, dim3(128), 0, as_stream(stream), q, nq, d, M, d / M,
-                               centroids, lut);
+        const int ds = d / M;
+        // compile-time dsub for the benchmarked shapes (round 6, profiles/r06_s36; bit-exact tests, r06_s37):
+        // 1000 queries, dsub 96 35.5 -> 34 us, 10,000 queries dsub 64 224 -> 197 us, dsub 48
+        // 33.5 -> 26.5 us
+        const int dsk = ds == 48 || ds == 64 || ds == 96 ? ds : 0;
+#define MIVQ_LUT_GO(L2V, DSV)                                                                                  \
+    hipLaunchKernelGGL((adc_lut_pk_kernel<L2V, DSV>), grid, dim3(128), 0, as_stream(stream), q, nq, d, M, ds, \
+                       centroids, lut)
+        const bool l2 = metric == MIVQ_METRIC_L2;
+        switch (dsk) {
+            case 48: if (l2) MIVQ_LUT_GO(true, 48); else MIVQ_LUT_GO(false, 48); break;
+            case 64: if (l2) MIVQ_LUT_GO(true, 64); else MIVQ_LUT_GO(false, 64); break;
+            case 96: if (l2) MIVQ_LUT_GO(true, 96); else MIVQ_LUT_GO(false, 96); break;
+            default: if (l2) MIVQ_LUT_GO(true, 0); else MIVQ_LUT_GO(false, 0); break;
+        }
+#undef MIVQ_LUT_GO
         return check_launch("adc_lut");
     }
     const size_t smem = (size_t)kLutQ * (d / M) * sizeof(float);

@@ -943,6 +943,33 @@ __global__ __launch_bounds__(kScanWaves * 64) void adc_qscan_kernel(
     }
 }
 
+// The rerank's first 64 entries all beat the empty list's +inf threshold: instead of ~28
+// sequential wave inserts (each a ballot and four cross-lane moves in a dependent chain) they are
+// sorted at once -- bitonic, 21 compare-exchange stages on (dist, id) -- and become the list
+// (R = 1, k <= 64: element e in lane e).  The k smallest pairs are unique, so the list equals the
+// one the inserts build.
+__device__ __forceinline__ void rr_seed(WaveTopK<1>& top, bool valid, float dv, uint32_t id, int k, int lane,
+                                        float& thr_d, uint32_t& thr_i) {
+    float d = valid ? dv : INFINITY;
+    uint32_t i = valid ? id : kNoId;
+#pragma unroll
+    for (int size = 2; size <= 64; size <<= 1) {
+#pragma unroll
+        for (int stride = size >> 1; stride > 0; stride >>= 1) {
+            const float od = __shfl_xor(d, stride);
+            const uint32_t oi = (uint32_t)__shfl_xor((int)i, stride);
+            const bool up = (lane & size) == 0 || size == 64;  // ascending run
+            const bool lower = (lane & stride) == 0;
+            const bool take = lower == up ? pair_less(od, oi, d, i) : pair_less(d, i, od, oi);
+            d = take ? od : d;
+            i = take ? oi : i;
+        }
+    }
+    top.d[0] = d;
+    top.id[0] = i;
+    top.kth(k, thr_d, thr_i);
+}
+
 // One wave per query: canonical fp32 distances of the listed rows, exact top-k, certificate.
 template <int R, int MC>
 __global__ __launch_bounds__(256) void adc_rerank_kernel(const float* __restrict__ lut, int64_t nq,
@@ -980,6 +1007,37 @@ __global__ __launch_bounds__(256) void adc_rerank_kernel(const float* __restrict
         __builtin_amdgcn_wave_barrier();
     }
     const int64_t total = (int64_t)parts * k1;
+    auto eval = [&](bool valid, const uint4 (&cw)[MC]) __attribute__((always_inline)) {
+        float dv = INFINITY;
+        if (valid) {
+            float t[M];
+#pragma unroll
+            for (int c = 0; c < MC; ++c) {
+                const uint32_t wd[4] = {cw[c].x, cw[c].y, cw[c].z, cw[c].w};
+#pragma unroll
+                for (int j = 0; j < 16; ++j)
+                    t[16 * c + j] = lq[(16 * c + j) * 256 + ((wd[j >> 2] >> (8 * (j & 3))) & 0xFFu)];
+            }
+            dv = 0.0f;
+#pragma unroll
+            for (int m = 0; m < M; ++m) dv += t[m];  // the canonical order
+            if (dv != dv) dv = INFINITY;
+        }
+        return dv;
+    };
+    auto offer = [&](bool first, bool valid, float dv, uint32_t id) __attribute__((always_inline)) {
+        // (round 6 split, profiling builds traced in r06_s39: 33 us per 1000 x 1M search, of which
+        // ~12.5 us were the sequential wave inserts -- the first step's now one sort, r06_s40)
+        if constexpr (R == 1) {
+            if (first) rr_seed(top, valid, dv, id, k, lane, thr_d, thr_i);
+            else top.offer(valid, dv, id, k, lane, thr_d, thr_i);
+        } else {
+            top.offer(valid, dv, id, k, lane, thr_d, thr_i);
+        }
+    };
+    // (round 6: ids and code rows by range-checked buffer loads in chunks of 8 steps -- all of a
+    // chunk's gathers in flight at once -- measured 26.5 -> 23.9 us here but neutral to 0.3 %
+    // slower end to end at M = 32 and the config #5 shape, r06_s41: not kept)
     // three-stage pipeline over the list in steps of 64 entries (round 6): the ids two steps
     // ahead and the code rows (which need those ids) one step ahead are in flight while a step
     // is evaluated, instead of an id load -> row gather -> lookups round trip per step
@@ -1006,25 +1064,7 @@ __global__ __launch_bounds__(256) void adc_rerank_kernel(const float* __restrict
         ld_row(id_nxt, cw_nxt);
         const uint32_t id = id_cur;
         const bool valid = id != kNoId;
-        float dv = INFINITY;
-        if (valid) {
-            uint4 cw[MC];
-#pragma unroll
-            for (int c = 0; c < MC; ++c) cw[c] = cw_cur[c];
-            float t[M];
-#pragma unroll
-            for (int c = 0; c < MC; ++c) {
-                const uint32_t wd[4] = {cw[c].x, cw[c].y, cw[c].z, cw[c].w};
-#pragma unroll
-                for (int j = 0; j < 16; ++j)
-                    t[16 * c + j] = lq[(16 * c + j) * 256 + ((wd[j >> 2] >> (8 * (j & 3))) & 0xFFu)];
-            }
-            dv = 0.0f;
-#pragma unroll
-            for (int m = 0; m < M; ++m) dv += t[m];  // the canonical order
-            if (dv != dv) dv = INFINITY;
-        }
-        top.offer(valid, dv, id, k, lane, thr_d, thr_i);
+        offer(e0 == 0, valid, eval(valid, cw_cur), id);
         id_cur = id_nxt;
         id_nxt = id_far;
 #pragma unroll
@@ -1270,6 +1310,7 @@ hipError_t launch_filtered(int M, const float* lut, int64_t nq, const uint8_t* c
     const dim3 rgrid((unsigned)ceil_div(nq, 4));
     const int lut16 = reinterpret_cast<uintptr_t>(lut) % 16 == 0;
     const size_t rsm = (size_t)4 * M * 256 * sizeof(float);  // four query LUTs: 64 / 128 KiB
+    // the buffer-load rerank needs 32-bit byte offsets into the codes and into the part lists
 #define MIVQ_RR(RR, MM)                                                                                              \
     {                                                                                                                \
         e = hipFuncSetAttribute((const void*)adc_rerank_kernel<RR, MM>, hipFuncAttributeMaxDynamicSharedMemorySize, \

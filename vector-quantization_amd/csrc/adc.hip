@@ -676,18 +676,25 @@ __global__ __launch_bounds__(256) void adc_qtab_kernel(const float* __restrict__
     uint32_t w[NWD];
 #pragma unroll
     for (int j = 0; j < NWD; ++j) w[j] = 0u;
+    // every load of the block's QB queries first (rows past nq clamped to the last query, their
+    // bytes zeroed below), then the arithmetic: one memory round trip instead of one per query
+    // behind the per-query branches
+    float lv[QB], mv[QB];
+    double dl[QB];
+    int bd[QB];
 #pragma unroll
     for (int qq = 0; qq < QB; ++qq) {
-        const int64_t qi = qb * QB + qq;
-        uint32_t v = 0u;
-        if (qi < nq) {
-            const AdcQStat st = qs[qi];
-            if (!st.bad) {
-                const double x = ((double)lut[(qi * M + m) * 256 + c] - (double)mins[qi * M + m]) / st.delta *
-                                 (1.0 - 8.881784197001252e-16);
-                v = x >= (double)qmax ? (uint32_t)qmax : x > 0.0 ? (uint32_t)floor(x) : 0u;
-            }
-        }
+        const int64_t qi = min(qb * QB + qq, nq - 1);
+        lv[qq] = lut[(qi * M + m) * 256 + c];
+        mv[qq] = mins[qi * M + m];
+        dl[qq] = qs[qi].delta;
+        bd[qq] = qs[qi].bad;
+    }
+#pragma unroll
+    for (int qq = 0; qq < QB; ++qq) {
+        const double x = ((double)lv[qq] - (double)mv[qq]) / dl[qq] * (1.0 - 8.881784197001252e-16);
+        uint32_t v = x >= (double)qmax ? (uint32_t)qmax : x > 0.0 ? (uint32_t)floor(x) : 0u;
+        if (qb * QB + qq >= nq || bd[qq]) v = 0u;
         const int r = qq & 3;
         w[qq >> 2] |= v << (8 * (((r & 1) << 1) | (r >> 1)));
     }
